@@ -1,0 +1,153 @@
+/*
+ * mvae.h — C ABI of libmvae, the MI355X (gfx950) training step of the "magic"
+ * asymmetric metric-VAE (reference: ag8/magic, class TangoEncoder).
+ *
+ * The reference has no FFI: its "operator API" is the Python class
+ * TangoEncoder(sess) driven through tf.Session.run (11a/vae.py:13,22) and fed by
+ * overlap_input.inputs() (11a/overlap_input.py:76). Each entry point below replaces
+ * one of those graph evaluations; the Python mirror of the reference interface
+ * (magic_amd/vae.py) binds them through ctypes. Plain pointers and sizes only:
+ * every float* argument is a DEVICE pointer owned by the caller unless stated.
+ *
+ *   reference call (file:line)                      -> entry point(s)
+ *   TangoEncoder.__init__  11a/vae.py:22-332         -> mvae_create (+ mvae_param_* for init)
+ *   partial_fit            11a/vae.py:385-411        -> mvae_train_step
+ *                                                      = mvae_forward, mvae_metric,
+ *                                                        mvae_backward, mvae_adam
+ *                                                      (split so a data-parallel host can
+ *                                                       all-reduce between the phases)
+ *   get_predictions        11a/vae.py:413-414        -> mvae_predict
+ *   transform              11a/vae.py:416-420        -> mvae_transform
+ *   generate               11a/vae.py:422-434        -> mvae_generate
+ *   reconstruct            11a/vae.py:436-440        -> mvae_reconstruct
+ *
+ * Errors: 0 = ok; <0 = invalid argument / configuration (MVAE_E*); >0 = hipError_t.
+ * No exception crosses the ABI; mvae_last_error() returns a message.
+ * Threading: one context per device per process; a context is not thread-safe;
+ * all work is enqueued on the caller's stream (hipStream_t passed as void*).
+ */
+#ifndef MVAE_H_
+#define MVAE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MVAE_ABI_VERSION 1
+#define MVAE_MAX_ENC 8
+
+enum { MVAE_OK = 0, MVAE_EINVAL = -1, MVAE_ECONFIG = -2, MVAE_ESTATE = -3 };
+enum { MVAE_ACT_TANH = 0, MVAE_ACT_ELU = 1 };                    /* 8c family : 11a */
+enum { MVAE_METRIC_COSINE = 0, MVAE_METRIC_SQDIFF = 1 };        /* 11a/constants.py:5-7 */
+enum { MVAE_PREC_F32 = 0, MVAE_PREC_BF16 = 1 };                 /* GEMM operand precision */
+
+/* Hyper-parameters the reference hard-codes in TangoEncoder.__init__ (11a/vae.py:30-65)
+ * and FLAGS (11a/constants.py:32,49,52,60). */
+typedef struct mvae_cfg {
+  int image_size;        /* H = W; D = H*W pixels per image                    */
+  int batch;             /* rows per call on this rank (FLAGS.BATCH_SIZE)      */
+  int global_batch;      /* rows over all ranks; losses/grads scale by 1/global */
+  int n_enc;             /* encoder depth (1..MVAE_MAX_ENC)                    */
+  int enc[MVAE_MAX_ENC]; /* encoder widths, 11a/vae.py:30                      */
+  int dec[2];            /* decoder widths, fixed [500,500] (11a/vae.py:36)    */
+  int latent;            /* L, 11a/vae.py:49                                   */
+  int act;               /* MVAE_ACT_*                                          */
+  int metric;            /* MVAE_METRIC_*                                       */
+  int reciprocal;        /* distance = 1/raw (11a/vae.py:307,309)              */
+  float deform_weight;   /* 10 (8c/vae.py:287) or 100 (11a/vae.py:293)         */
+  float lr[2];           /* [cost optimizer, metric optimizer]                 */
+  float beta1, beta2, epsilon; /* TF AdamOptimizer defaults .9/.999/1e-8       */
+  int precision;         /* MVAE_PREC_*                                         */
+  uint64_t seed;         /* counter-based N(0,1) stream for eps when not given */
+} mvae_cfg;
+
+typedef struct mvae_ctx mvae_ctx;
+
+/* Named views into context-owned device memory. */
+enum {
+  MVAE_KIND_PARAM = 0, MVAE_KIND_GRAD1 = 1, MVAE_KIND_GRAD2 = 2,
+  MVAE_KIND_M1 = 3, MVAE_KIND_V1 = 4, MVAE_KIND_M2 = 5, MVAE_KIND_V2 = 6
+};
+typedef struct mvae_tensor {
+  char name[48];    /* reference variable meaning, e.g. "enc_h0_W", "dec_out_mean_b" */
+  float* data;      /* device pointer of element [0][0]                               */
+  int rows, cols;   /* logical shape (a bias is rows=1)                                */
+  int ld;           /* row stride in elements                                          */
+  int trained_by;   /* bit0: cost optimizer, bit1: metric optimizer, 0: dead variable  */
+} mvae_tensor;
+
+/* Flat buffers (for checkpoints and the data-parallel gradient all-reduce). */
+enum {
+  MVAE_BUF_PARAMS = 0,   /* all trained parameters (augmented [W;b] blocks)            */
+  MVAE_BUF_GRADS = 1,    /* [g1 (all trained) | g2 (encoder)] — the all-reduce bucket  */
+  MVAE_BUF_ADAM = 2,     /* [m1 | v1 | m2 | v2]                                        */
+  MVAE_BUF_LOSSES = 3,   /* float[8]: cost, training_loss, r_l, l_l, d_l (rank-local
+                            partial sums scaled by 1/global_batch; global after a sum)  */
+  MVAE_BUF_COLSQ = 4,    /* float[2L]: sum_b z_lock^2, sum_b z_key^2 (cosine metric)    */
+  MVAE_BUF_COLDOT = 5,   /* float[L]:  sum_b draw_b n_lock n_key     (cosine metric)    */
+  MVAE_BUF_DIST = 6,     /* float[B]: distance of the last forward                      */
+  MVAE_BUF_GRADS_DEC = 7,/* decoder slice of g1 (ready first in mvae_backward)         */
+  MVAE_BUF_DEAD = 8,     /* the never-trained decoder log-sigma variables               */
+  MVAE_BUF_EPS = 9       /* float[3,B,L]: eps of the last forward (given or generated)  */
+};
+
+int mvae_abi_version(void);
+int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out);
+int mvae_destroy(mvae_ctx* ctx);
+const char* mvae_last_error(mvae_ctx* ctx);   /* ctx may be NULL (creation errors) */
+
+int mvae_param_count(mvae_ctx* ctx);
+int mvae_param_info(mvae_ctx* ctx, int kind, int index, mvae_tensor* out);
+int mvae_buffer(mvae_ctx* ctx, int which, float** ptr, size_t* count);
+/* Optimizer step counters (TF beta1_power/beta2_power, kept on the host in fp32). */
+int mvae_get_step(mvae_ctx* ctx, int64_t* t1, int64_t* t2);
+int mvae_set_step(mvae_ctx* ctx, int64_t t1, int64_t t2);
+/* Re-derive the bf16 shadow weights from the fp32 masters (after an external write). */
+int mvae_sync_params(mvae_ctx* ctx, void* stream);
+
+/* ---- training step, phase by phase --------------------------------------------- */
+/* x: [B, 3*D] f32 HWC-interleaved (lock, rotated lock, key), 11a/overlap_input.py:117-119.
+ * eps: [3, B, L] f32 in the reference's draw order (lock, rotated, key), or NULL to draw
+ * from the context's counter-based generator (seed, call counter).                   */
+int mvae_forward(mvae_ctx* ctx, const float* x, const float* eps, void* stream);
+/* areas: [B] f32. Needs MVAE_BUF_COLSQ summed over ranks (cosine) before the call.    */
+int mvae_metric(mvae_ctx* ctx, const float* areas, void* stream);
+/* Needs MVAE_BUF_COLDOT summed over ranks (cosine). Writes MVAE_BUF_GRADS.           */
+int mvae_backward(mvae_ctx* ctx, void* stream);
+/* Both TF ApplyAdam updates from MVAE_BUF_GRADS (theta -= d1(g1) + d2(g2)).           */
+int mvae_adam(mvae_ctx* ctx, void* stream);
+/* Single-GPU partial_fit: all four phases. losses_out: device float[5] or NULL;
+ * dist_out: device float[B] or NULL.                                                  */
+int mvae_train_step(mvae_ctx* ctx, const float* x, const float* areas, const float* eps,
+                    float* losses_out, float* dist_out, void* stream);
+
+/* ---- inference surface ------------------------------------------------------------ */
+int mvae_predict(mvae_ctx* ctx, const float* x, const float* eps, float* dist_out, void* stream);
+int mvae_transform(mvae_ctx* ctx, const float* x, float* zmean_out, void* stream);
+int mvae_reconstruct(mvae_ctx* ctx, const float* x, const float* eps, float* y_out, void* stream);
+/* z: [n, L] (n <= B) -> y: [n, D] */
+int mvae_generate(mvae_ctx* ctx, const float* z, int n, float* y_out, void* stream);
+
+/* ---- diagnostics ------------------------------------------------------------------ */
+/* HIP-event timing of named regions (one GEMM incl. its split-K reduction, or one
+ * bandwidth kernel group), recorded on the launch stream while enabled.               */
+int mvae_timing_enable(mvae_ctx* ctx, int on);
+int mvae_timing_regions(mvae_ctx* ctx);
+const char* mvae_timing_name(mvae_ctx* ctx, int region);
+int mvae_timing_read(mvae_ctx* ctx, int region, double* total_ms, int64_t* count);
+int mvae_timing_reset(mvae_ctx* ctx);
+/* One GEMM of the step's kernel family: C[M,N] = epi(A[M,K] B[K,N]); A stored [M][K]
+ * (at=0) or [K][M] (at=1), B stored [K][N] (bt=0) or [N][K] (bt=1). epi: 0 store,
+ * 1 act (act: 0 tanh, 1 elu), 2 C = acc * act'(aux), 4 sigmoid. split_k: 0 = planner's
+ * choice. Workspace is allocated and freed inside (synchronous; tests only).           */
+int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int at, const float* B, int ldb,
+                    int bt, float* C, int ldc, int epi, int act, const float* aux, int ld_aux,
+                    void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MVAE_H_ */

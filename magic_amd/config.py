@@ -1,0 +1,100 @@
+"""Hyper-parameter presets of the reference's metric-VAE lineage and the
+BASELINE.json run configurations.
+
+The reference hard-codes these in ``TangoEncoder.__init__`` (``11a/vae.py:30-65``,
+``8c/vae.py:30-63``) and in ``FLAGS`` (``11a/constants.py:32,52,60``); here they are one
+dataclass so every preset is reachable by name.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Optional, Tuple
+
+
+@dataclasses.dataclass
+class MVAEConfig:
+    image_size: int = 100
+    batch: int = 64
+    global_batch: Optional[int] = None       # None -> batch (single rank)
+    enc: Tuple[int, ...] = (500, 500, 500, 500)
+    dec: Tuple[int, int] = (500, 500)
+    latent: int = 20
+    act: str = "tanh"
+    metric: str = "cosine"
+    reciprocal: bool = False
+    deform_weight: float = 10.0
+    lr: Tuple[float, float] = (1e-4, 1e-6)
+    beta1: float = 0.9
+    beta2: float = 0.999
+    epsilon: float = 1e-8
+    precision: str = "f32"
+    seed: int = 2
+
+    @property
+    def D(self) -> int:
+        return self.image_size * self.image_size
+
+    @property
+    def gbatch(self) -> int:
+        return self.global_batch or self.batch
+
+    def replace(self, **kw) -> "MVAEConfig":
+        return dataclasses.replace(self, **kw)
+
+    def flops_per_pair(self) -> float:
+        """Algorithmic FLOPs of one training pair: 3 encoder forwards,
+        1 decoder forward, decoder backward, 4 encoder backward passes (lock x2, rot, key)."""
+        D, L = self.D, self.latent
+        widths = [D] + list(self.enc)
+        enc_fwd = sum(2 * a * b for a, b in zip(widths[:-1], widths[1:])) + 2 * self.enc[-1] * 2 * L
+        dec_layers = [(L, self.dec[0]), (self.dec[0], self.dec[1]), (self.dec[1], D)]
+        dec_fwd = sum(2 * a * b for a, b in dec_layers)
+        dec_bwd = 2 * dec_fwd  # wgrad + dgrad (the dgrad into z is counted, cheap)
+        # encoder backward per pass: wgrad of every layer + dgrad of every layer but the first
+        enc_w = enc_fwd
+        enc_d = enc_fwd - 2 * D * self.enc[0]
+        enc_bwd = 4 * (enc_w + enc_d)
+        return float(3 * enc_fwd + dec_fwd + dec_bwd + enc_bwd)
+
+
+# SURVEY.md §2.3 (reference IMAGE_SIZE is 200; BASELINE runs use 100 — pass image_size=)
+PRESETS = {
+    "8c": dict(enc=(500, 500, 500, 500), latent=20, act="tanh", deform_weight=10.0,
+               lr=(1e-4, 1e-6), metric="cosine", reciprocal=False),
+    "8d": dict(enc=(500, 500, 500, 500), latent=200, act="tanh", deform_weight=10.0,
+               lr=(1e-4, 1e-6), metric="cosine", reciprocal=False),
+    "8e": dict(enc=(500, 500, 500, 500), latent=2000, act="tanh", deform_weight=10.0,
+               lr=(1e-4, 1e-6), metric="cosine", reciprocal=False),
+    "8f": dict(enc=(10000, 5000, 1000, 500), latent=2000, act="tanh", deform_weight=10.0,
+               lr=(1e-4, 1e-6), metric="cosine", reciprocal=False),
+    "9a": dict(enc=(500, 500, 500, 500), latent=2, act="tanh", deform_weight=10.0,
+               lr=(1e-4, 1e-6), metric="cosine", reciprocal=True),
+    "10a": dict(enc=(500, 500, 500, 500), latent=80, act="tanh", deform_weight=10.0,
+                lr=(1e-4, 1e-8), metric="cosine", reciprocal=True),
+    "11a": dict(enc=(500, 500), latent=80, act="elu", deform_weight=100.0,
+                lr=(1e-6, 1e-8), metric="sqdiff", reciprocal=True),
+    "shapes": dict(enc=(500, 500), latent=200, act="tanh", deform_weight=100.0,
+                   lr=(1e-6, 1e-8), metric="sqdiff", reciprocal=True),
+}
+PRESET_BATCH = {"8c": 100, "8d": 100, "8e": 100, "8f": 100, "9a": 24, "10a": 24, "11a": 24,
+                "shapes": 24}
+
+
+def preset(name: str, image_size: int = 100, batch: Optional[int] = None, **kw) -> MVAEConfig:
+    p = dict(PRESETS[name])
+    p.update(kw)
+    return MVAEConfig(image_size=image_size, batch=batch or PRESET_BATCH[name], **p)
+
+
+# BASELINE.json "configs" 
+def baseline_config(cid: str) -> MVAEConfig:
+    cid = cid.upper()
+    if cid == "C1":
+        return preset("8c", batch=64)
+    if cid == "C2":
+        return preset("8c", batch=4096)
+    if cid in ("C3", "C4"):
+        return preset("8d", batch=8192)
+    if cid == "C5":
+        return preset("8e", batch=8192, metric="sqdiff", reciprocal=True)
+    raise KeyError(cid)

@@ -1,0 +1,394 @@
+// fp32-input MFMA GEMM for gfx950 (v_mfma_f32_32x32x2_f32: exact fp32, k-ordered fma chain)
+// with the fused epilogues of the metric-VAE step.
+//
+// C[M,N] = A[M,K] * B[K,N], A stored row-major [M][K] or transposed [K][M] (at),
+// B stored [K][N] or transposed [N][K] (bt). Every bias is folded into the GEMM: activation
+// buffers carry a constant ones column and each parameter block is the augmented [W; b]
+// (rows K+1), so forward = one GEMM, and the weight gradient of [W; b] = one GEMM whose M
+// includes the ones column (the bias gradient is its last row).
+//
+// Tile 128x128x32, 256 threads = 4 waves in 2x2, each wave 64x64 = 2x2 MFMA 32x32 tiles.
+// LDS tiles are k-major ([BK][BM+pad]) so every fragment read is a conflict-free ds_read_b32
+// at consecutive addresses; the register-staged global loader transposes operands whose
+// global layout is k-contiguous (pad 1 -> conflict-free transposing ds_write_b32) and copies
+// m-/n-contiguous operands with ds_write_b128 (pad 4). Double-buffered LDS, one barrier per
+// k-tile, next tile's global loads issued before the MFMAs of the current one.
+// Blocks are remapped so that the column tiles of one row panel share an XCD (L2 reuse of A).
+// Split-K (for small grids) writes fp32 partial slabs that a second kernel sums in a fixed
+// order and passes through the epilogue: results are deterministic run to run.
+#include "mvae_internal.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace mvae {
+namespace {
+
+constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct Params {
+  int M, N, K;
+  const float* A; int lda;
+  const float* B; int ldb;
+  float* C; int ldc;
+  long long sA, sB, sC;     // batch strides
+  int batch, split, kchunk;
+  int ntm, ntn;
+  GemmEpi epi;
+};
+
+__device__ __forceinline__ float act_f(float v, int act) {
+  if (act == ACT_TANH) return tanhf(v);
+  return v < 0.f ? expf(v) - 1.f : v;  // TF elu: exp(x) - 1 for x < 0
+}
+__device__ __forceinline__ float dact_f(float g, float y, int act) {
+  if (act == ACT_TANH) return g * (1.f - y * y);  // TF TanhGrad
+  return y < 0.f ? g * (y + 1.f) : g;              // TF EluGrad (on the output)
+}
+__device__ __forceinline__ float sigmoid_f(float v) { return 1.f / (1.f + expf(-v)); }
+
+// bijective XCD remap: consecutive logical tiles land on the same XCD (blockIdx % 8 group)
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = b & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+template <bool KCONTIG, int SLD, int ROWS>
+struct TileLoader;
+
+// operand whose global layout is k-contiguous: [rows][K] -> LDS [BK][rows] (transpose)
+template <int SLD, int ROWS>
+struct TileLoader<true, SLD, ROWS> {
+  float4 r[4];
+  __device__ __forceinline__ void load(const float* __restrict__ g, int ld, int row0, int nrows,
+                                       int k0, int kend, int tid) {
+    const bool kfull = k0 + BK <= kend;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = tid + NT * j;
+      const int row = c >> 3, kq = c & 7;
+      int gr = row0 + row;
+      gr = gr < nrows ? gr : nrows - 1;
+      const int gk = k0 + 4 * kq;
+      const float* p = g + (size_t)gr * ld + gk;
+      if (kfull) {
+        r[j] = *reinterpret_cast<const float4*>(p);
+      } else {
+        r[j].x = gk + 0 < kend ? p[0] : 0.f;
+        r[j].y = gk + 1 < kend ? p[1] : 0.f;
+        r[j].z = gk + 2 < kend ? p[2] : 0.f;
+        r[j].w = gk + 3 < kend ? p[3] : 0.f;
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float* s, int tid) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = tid + NT * j;
+      const int row = c >> 3, kq = c & 7;
+      float* q = s + (4 * kq) * SLD + row;
+      q[0] = r[j].x; q[SLD] = r[j].y; q[2 * SLD] = r[j].z; q[3 * SLD] = r[j].w;
+    }
+  }
+};
+
+// operand whose global layout is row(m/n)-contiguous: [K][rows] -> LDS [BK][rows] (copy)
+template <int SLD, int ROWS>
+struct TileLoader<false, SLD, ROWS> {
+  float4 r[4];
+  __device__ __forceinline__ void load(const float* __restrict__ g, int ld, int row0, int nrows,
+                                       int k0, int kend, int tid) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = tid + NT * j;
+      const int k = c >> 5, rq = c & 31;
+      const int gk = k0 + k;
+      const int gr = row0 + 4 * rq;
+      if (gk < kend) {
+        const float* p = g + (size_t)gk * ld + gr;
+        if (gr + 3 < nrows) {
+          r[j] = *reinterpret_cast<const float4*>(p);
+        } else {
+          r[j].x = gr + 0 < nrows ? p[0] : 0.f;
+          r[j].y = gr + 1 < nrows ? p[1] : 0.f;
+          r[j].z = gr + 2 < nrows ? p[2] : 0.f;
+          r[j].w = gr + 3 < nrows ? p[3] : 0.f;
+        }
+      } else {
+        r[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  }
+  __device__ __forceinline__ void store(float* s, int tid) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = tid + NT * j;
+      const int k = c >> 5, rq = c & 31;
+      *reinterpret_cast<float4*>(s + k * SLD + 4 * rq) = r[j];
+    }
+  }
+};
+
+template <bool AT, bool BT, int EPI>
+__global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(Params p) {
+  constexpr bool A_KC = !AT;  // A stored [M][K] -> k-contiguous
+  constexpr bool B_KC = BT;   // B stored [N][K] -> k-contiguous
+  constexpr int SA = A_KC ? BM + 1 : BM + 4;
+  constexpr int SB = B_KC ? BN + 1 : BN + 4;
+  constexpr int A_TILE = BK * SA, B_TILE = BK * SB;
+  __shared__ __attribute__((aligned(16))) float smem[2 * (A_TILE + B_TILE)];
+  float* As = smem;
+  float* Bs = smem + 2 * A_TILE;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  const int tiles = p.ntm * p.ntn;
+  const int nwg = tiles * p.batch * p.split;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  const int z = t / tiles;
+  const int rem = t - z * tiles;
+  const int mt = rem / p.ntn, nt = rem - mt * p.ntn;
+  const int bi = z / p.split, si = z - bi * p.split;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const int ks = si * p.kchunk;
+  const int ke = min(p.K, ks + p.kchunk);
+
+  const float* __restrict__ A = p.A + bi * p.sA;
+  const float* __restrict__ Bm = p.B + bi * p.sB;
+
+  TileLoader<A_KC, SA, BM> la;
+  TileLoader<B_KC, SB, BN> lb;
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = ks < ke ? (ke - ks + BK - 1) / BK : 0;
+  if (nk > 0) {
+    la.load(A, p.lda, m0, p.M, ks, ke, tid);
+    lb.load(Bm, p.ldb, n0, p.N, ks, ke, tid);
+    la.store(As, tid);
+    lb.store(Bs, tid);
+  }
+  __syncthreads();
+
+  const int fr = lane & 31, fk = lane >> 5;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      la.load(A, p.lda, m0, p.M, ks + (kt + 1) * BK, ke, tid);
+      lb.load(Bm, p.ldb, n0, p.N, ks + (kt + 1) * BK, ke, tid);
+    }
+    const float* as = As + cur * A_TILE + wm * 64 + fr;
+    const float* bs = Bs + cur * B_TILE + wn * 64 + fr;
+#pragma unroll
+    for (int kk = 0; kk < BK / 2; ++kk) {
+      const int k = 2 * kk + fk;
+      const float a0 = as[k * SA], a1 = as[k * SA + 32];
+      const float b0 = bs[k * SB], b1 = bs[k * SB + 32];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (more) {
+      la.store(As + (cur ^ 1) * A_TILE, tid);
+      lb.store(Bs + (cur ^ 1) * B_TILE, tid);
+    }
+    __syncthreads();
+  }
+
+  // ---------------------------------------------------------------- epilogue
+  // C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+  float* __restrict__ C = p.C + (size_t)z * p.sC;  // z = bi*split + si (slab) or bi (split==1)
+  const int rbase = m0 + wm * 64 + 4 * fk;
+  const int cbase = n0 + wn * 64 + fr;
+  if constexpr (EPI == EPI_BCE) {
+    const GemmEpi& e = p.epi;
+    float* red = smem;  // reuse LDS: [2][BM] row sums of the two column waves
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + mi * 32 + (r & 3) + 8 * (r >> 2);
+        float rs = 0.f;
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          const int col = cbase + ni * 32;
+          if (row < p.M && col < p.N) {
+            const float yv = sigmoid_f(acc[mi][ni][r]);
+            const float xv = e.x[(size_t)row * e.ldx + col];
+            // -log(y^x (1-y)^(1-x)) with TF pow(0,0) = 1 (no epsilon), 11a/vae.py:266-269
+            float term = 0.f;
+            if (xv != 0.f) term += xv * logf(yv);
+            if (xv != 1.f) term += (1.f - xv) * logf(1.f - yv);
+            rs += term;
+            C[(size_t)row * p.ldc + col] = (yv - xv) * e.scale;
+            if (e.y) e.y[(size_t)row * e.ldy + col] = yv;
+          }
+        }
+#pragma unroll
+        for (int off = 16; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
+        if (fr == 0) red[wn * BM + (row - m0)] = rs;  // lanes 0 and 32
+      }
+    }
+    __syncthreads();
+    if (tid < BM && m0 + tid < p.M) {
+      e.rowpart[(size_t)(m0 + tid) * p.ntn + nt] = -(red[tid] + red[BM + tid]);
+    }
+    return;
+  } else {
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + mi * 32 + (r & 3) + 8 * (r >> 2);
+        if (row >= p.M) continue;
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          const int col = cbase + ni * 32;
+          if (col >= p.N) continue;
+          float v = acc[mi][ni][r];
+          if constexpr (EPI == EPI_ACT) v = act_f(v, p.epi.act);
+          if constexpr (EPI == EPI_SIGMOID) v = sigmoid_f(v);
+          if constexpr (EPI == EPI_DACT) {
+            const int ar = row >= p.epi.remap_split ? row - p.epi.remap_shift : row;
+            v = dact_f(v, p.epi.aux[(size_t)ar * p.epi.ld_aux + col], p.epi.act);
+          }
+          C[(size_t)row * p.ldc + col] = v;
+        }
+      }
+    }
+  }
+}
+
+// sum split-K slabs in fixed order and apply the epilogue
+template <int EPI>
+__global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, int M, int N,
+                                     float* __restrict__ C, int ldc, long long sC, GemmEpi e) {
+  const int bi = blockIdx.z;
+  const long long slab = (long long)M * N;
+  const float* w = ws + (size_t)bi * split * slab;
+  float* c = C + bi * sC;
+  const long long total = slab;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    float v = 0.f;
+    for (int s = 0; s < split; ++s) v += w[s * slab + i];
+    const int row = (int)(i / N), col = (int)(i - (long long)row * N);
+    if constexpr (EPI == EPI_ACT) v = act_f(v, e.act);
+    if constexpr (EPI == EPI_SIGMOID) v = sigmoid_f(v);
+    if constexpr (EPI == EPI_DACT) {
+      const int ar = row >= e.remap_split ? row - e.remap_shift : row;
+      v = dact_f(v, e.aux[(size_t)ar * e.ld_aux + col], e.act);
+    }
+    c[(size_t)row * ldc + col] = v;
+  }
+}
+
+template <bool AT, bool BT, int EPI>
+hipError_t launch_t(const Params& p, hipStream_t st) {
+  const int nwg = p.ntm * p.ntn * p.batch * p.split;
+  hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, EPI>), dim3(nwg), dim3(NT), 0, st, p);
+  return hipGetLastError();
+}
+
+template <int EPI>
+hipError_t launch_layout(const Params& p, bool at, bool bt, hipStream_t st) {
+  if (!at && !bt) return launch_t<false, false, EPI>(p, st);
+  if (at && !bt) return launch_t<true, false, EPI>(p, st);
+  if (!at && bt) return launch_t<false, true, EPI>(p, st);
+  return launch_t<true, true, EPI>(p, st);
+}
+
+}  // namespace
+
+int gemm_bce_nblk(int N) { return (N + BN - 1) / BN; }
+
+int gemm_plan_split(const GemmDesc& d, size_t max_ws) {
+  if (d.epi.mode == EPI_BCE || d.epi.mode == EPI_SIGMOID) return 1;
+  const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
+  const long long tiles = (long long)ntm * ntn * d.batch;
+  const int ktiles = (d.K + BK - 1) / BK;
+  // Throughput model: each CU works through ceil(WGs/256) workgroups (two co-resident WGs
+  // overlap each other's stalls but share the MFMA pipes), each WG costs its k-tiles plus a
+  // fixed prologue/epilogue; split-K adds the slab round trip and one reduction launch.
+  const double cus = 256.0;
+  const double t_ktile = 1.75e-6;  // one 128x128x32 fp32 k-tile at the CU's MFMA rate
+  double best = 1e30;
+  int best_s = 1;
+  for (int s = 1; s <= 32; ++s) {
+    if (s > 1 && ktiles / s < 4) break;
+    if (s > 1 && (size_t)d.batch * s * d.M * d.N > max_ws) break;
+    const double rounds = std::ceil(tiles * s / cus);
+    double t = rounds * ((double)ktiles / s + 2.0) * t_ktile;
+    if (s > 1) t += (double)d.batch * s * d.M * d.N * 8.0 / 4.5e12 + 4e-6;
+    if (t < best * 0.97) { best = t; best_s = s; }
+  }
+  return best_s;
+}
+
+size_t gemm_workspace_elems(const GemmDesc& d) {
+  const int s = gemm_plan_split(d, ~size_t(0));
+  return s > 1 ? (size_t)d.batch * s * d.M * d.N : 0;
+}
+
+hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t st) {
+  if (d.M <= 0 || d.N <= 0) return hipSuccess;
+  Params p;
+  p.M = d.M; p.N = d.N; p.K = d.K;
+  p.A = d.A; p.lda = d.lda; p.B = d.B; p.ldb = d.ldb;
+  p.sA = d.sA; p.sB = d.sB;
+  p.batch = d.batch;
+  p.ntm = (d.M + BM - 1) / BM; p.ntn = (d.N + BN - 1) / BN;
+  p.epi = d.epi;
+  const int split = gemm_plan_split(d, ws ? ws_elems : 0);
+  p.split = split;
+  const int ktiles = (d.K + BK - 1) / BK;
+  p.kchunk = ((ktiles + split - 1) / split) * BK;
+  if (split == 1) {
+    p.C = d.C; p.ldc = d.ldc; p.sC = d.sC;
+    switch (d.epi.mode) {
+      case EPI_STORE: return launch_layout<EPI_STORE>(p, d.at, d.bt, st);
+      case EPI_ACT: return launch_layout<EPI_ACT>(p, d.at, d.bt, st);
+      case EPI_DACT: return launch_layout<EPI_DACT>(p, d.at, d.bt, st);
+      case EPI_BCE: return launch_layout<EPI_BCE>(p, d.at, d.bt, st);
+      case EPI_SIGMOID: return launch_layout<EPI_SIGMOID>(p, d.at, d.bt, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
+  // split-K: raw slabs [batch][split][M][N], then ordered reduction + epilogue
+  p.C = ws; p.ldc = d.N; p.sC = (long long)d.M * d.N;
+  hipError_t err = launch_layout<EPI_STORE>(p, d.at, d.bt, st);
+  if (err != hipSuccess) return err;
+  const long long total = (long long)d.M * d.N;
+  int grid = (int)std::min<long long>((total + 255) / 256, 2048);
+  dim3 g(grid, 1, d.batch);
+  switch (d.epi.mode) {
+    case EPI_STORE:
+      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_STORE>, g, dim3(256), 0, st, ws, split, d.M, d.N, d.C, d.ldc, d.sC, d.epi);
+      break;
+    case EPI_ACT:
+      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_ACT>, g, dim3(256), 0, st, ws, split, d.M, d.N, d.C, d.ldc, d.sC, d.epi);
+      break;
+    case EPI_DACT:
+      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_DACT>, g, dim3(256), 0, st, ws, split, d.M, d.N, d.C, d.ldc, d.sC, d.epi);
+      break;
+    case EPI_SIGMOID:
+      hipLaunchKernelGGL(splitk_reduce_kernel<EPI_SIGMOID>, g, dim3(256), 0, st, ws, split, d.M, d.N, d.C, d.ldc, d.sC, d.epi);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace mvae

@@ -1,0 +1,769 @@
+// libmvae C ABI: context, parameter layout and the training-step schedule.
+//
+// HBM layout (all fp32, row-major, every row stride a multiple of 4 floats):
+//   theta  = [enc blocks | head | dec blocks], each block the augmented [W; b] of one layer
+//            ((fan_in+1) x fan_out; the head block is [W_mean W_logsigma; b_mean b_logsigma]).
+//   grads  = [g1 (same layout as theta) | g2 (encoder slice)] — ONE all-reduce bucket.
+//   adam   = [m1 | v1 | m2 | v2].
+//   Activation buffers carry a constant ones column after the last feature so every GEMM
+//   folds its bias (see gemm_f32.hip). Stacked encoder rows: [rot | lock | key] (3B),
+//   backward rows [rot:g1 | lock:g1 | lock:g2 | key:g2] (4B).
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/mvae.h"
+#include "mvae_internal.h"
+
+using namespace mvae;
+
+namespace {
+
+struct Block {
+  size_t off = 0;  // element offset in theta / g1
+  int K = 0, N = 0;
+};
+
+inline int round4(int v) { return (v + 3) & ~3; }
+inline size_t align64(size_t v) { return (v + 63) & ~size_t(63); }
+
+}  // namespace
+
+struct mvae_ctx {
+  mvae_cfg cfg{};
+  int device = 0;
+  int B = 0, D = 0, L = 0, nenc = 0, d0 = 0, d1 = 0;
+  float inv_bg = 1.f;
+  int ldx = 0, ldz = 0, ld_d1 = 0, ld_d2 = 0, ld_u = 0, lddz = 0, nblk = 0, nchunk = 0;
+  std::vector<int> ldh;
+  // parameters
+  std::vector<Block> enc;
+  Block head, v1, v2, vo;
+  size_t n_all = 0, n_enc = 0;
+  float* theta = nullptr;
+  float* grads = nullptr;
+  float* adam = nullptr;
+  float* dead = nullptr;
+  // activations / workspaces
+  float* xs = nullptr;
+  std::vector<float*> H;
+  float *ms = nullptr, *z = nullptr, *a1 = nullptr, *a2 = nullptr, *du = nullptr;
+  float *rowpart = nullptr, *rowvals = nullptr, *dist = nullptr, *draw = nullptr, *losses = nullptr;
+  float *colsq = nullptr, *coldot = nullptr, *cspart = nullptr, *eps = nullptr;
+  float *dzd2 = nullptr, *dzd1 = nullptr, *dzdec = nullptr, *dhead = nullptr, *dz[2] = {nullptr, nullptr};
+  float* zgen = nullptr;
+  float* ws = nullptr;
+  size_t ws_elems = 0;
+  std::vector<void*> allocs;
+  // schedule (each GEMM tagged with its timing region)
+  std::vector<GemmDesc> fwd_enc;  // encoder layers + head
+  GemmDesc f_d1, f_d2, f_out;
+  std::vector<GemmDesc> bwd_dec;  // W_out, D_out, W_d2, D_d2, W_d1, D_d1
+  std::vector<GemmDesc> bwd_enc;  // W_head, D_head, (W_i, D_i)..., W_0
+  std::vector<int> fwd_enc_r, bwd_dec_r, bwd_enc_r;
+  int f_d1_r = 0, f_d2_r = 0, f_out_r = 0;
+  // HIP-event timing regions (diagnostics / bench roofline)
+  std::vector<std::string> region_names;
+  std::vector<double> region_ms;
+  std::vector<int64_t> region_n;
+  struct Pending { int region; hipEvent_t a, b; };
+  std::vector<Pending> pending;
+  std::vector<hipEvent_t> event_pool;
+  bool timing = false;
+  // optimizer state (TF beta1_power / beta2_power are fp32 variables)
+  int64_t t1 = 0, t2 = 0;
+  float b1p[2] = {0, 0}, b2p[2] = {0, 0};
+  uint64_t rng_counter = 0;
+  int phase = 0;  // 0 idle, 1 forward done, 2 metric done, 3 backward done
+  std::string err;
+};
+
+static thread_local std::string g_create_err;
+
+#define MV_CHECK(expr)                                                              \
+  do {                                                                              \
+    hipError_t e_ = (expr);                                                         \
+    if (e_ != hipSuccess) {                                                         \
+      ctx->err = std::string(#expr) + ": " + hipGetErrorString(e_);                 \
+      return (int)e_;                                                               \
+    }                                                                               \
+  } while (0)
+
+static int fail(mvae_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg; else g_create_err = msg;
+  return code;
+}
+
+static hipError_t dalloc(mvae_ctx* ctx, float** p, size_t n) {
+  void* q = nullptr;
+  hipError_t e = hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(float));
+  if (e != hipSuccess) return e;
+  ctx->allocs.push_back(q);
+  *p = static_cast<float*>(q);
+  return hipMemset(q, 0, std::max<size_t>(n, 1) * sizeof(float));
+}
+
+static hipError_t ones_column(float* base, int ld, int col, int rows) {
+  std::vector<float> one(rows, 1.f);
+  return hipMemcpy2D(base + col, (size_t)ld * sizeof(float), one.data(), sizeof(float), sizeof(float),
+                     rows, hipMemcpyHostToDevice);
+}
+
+static GemmDesc gd(int M, int N, int K, const float* A, int lda, bool at, const float* Bm, int ldb,
+                   bool bt, float* C, int ldc, int mode = EPI_STORE) {
+  GemmDesc d;
+  d.M = M; d.N = N; d.K = K; d.A = A; d.lda = lda; d.at = at; d.B = Bm; d.ldb = ldb; d.bt = bt;
+  d.C = C; d.ldc = ldc; d.epi.mode = mode;
+  return d;
+}
+
+static int region(mvae_ctx* c, const std::string& name) {
+  for (size_t i = 0; i < c->region_names.size(); ++i)
+    if (c->region_names[i] == name) return (int)i;
+  c->region_names.push_back(name);
+  c->region_ms.push_back(0.0);
+  c->region_n.push_back(0);
+  return (int)c->region_names.size() - 1;
+}
+
+static hipEvent_t take_event(mvae_ctx* c) {
+  if (!c->event_pool.empty()) {
+    hipEvent_t e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+// RAII: records a start/stop event pair around one region on the launch stream
+struct TimeScope {
+  mvae_ctx* c; int r; hipStream_t st; hipEvent_t a = nullptr;
+  TimeScope(mvae_ctx* c_, int r_, hipStream_t st_) : c(c_), r(r_), st(st_) {
+    if (c->timing) { a = take_event(c); (void)hipEventRecord(a, st); }
+  }
+  ~TimeScope() {
+    if (a) {
+      hipEvent_t b = take_event(c);
+      (void)hipEventRecord(b, st);
+      c->pending.push_back({r, a, b});
+    }
+  }
+};
+
+static void build_schedule(mvae_ctx* c) {
+  const int B = c->B, L = c->L, n = c->nenc, act = c->cfg.act;
+  float* th = c->theta;
+  float* g1 = c->grads;
+  const long long n_all = (long long)c->n_all;
+  // ---- forward: encoder on the stacked 3B rows
+  c->fwd_enc.clear();
+  for (int i = 0; i < n; ++i) {
+    const float* A = i == 0 ? c->xs : c->H[i - 1];
+    const int lda = i == 0 ? c->ldx : c->ldh[i - 1];
+    GemmDesc d = gd(3 * B, c->enc[i].N, c->enc[i].K + 1, A, lda, false, th + c->enc[i].off,
+                    c->enc[i].N, false, c->H[i], c->ldh[i], EPI_ACT);
+    d.epi.act = act;
+    c->fwd_enc.push_back(d);
+    c->fwd_enc_r.push_back(region(c, "enc_fwd_" + std::to_string(i)));
+  }
+  c->fwd_enc.push_back(gd(3 * B, 2 * L, c->head.K + 1, c->H[n - 1], c->ldh[n - 1], false,
+                          th + c->head.off, 2 * L, false, c->ms, 2 * L));
+  c->fwd_enc_r.push_back(region(c, "head_fwd"));
+  c->f_d1_r = region(c, "dec_fwd_1");
+  c->f_d2_r = region(c, "dec_fwd_2");
+  c->f_out_r = region(c, "dec_fwd_out_bce");
+  for (const char* nm : {"dec_bwd_w_out", "dec_bwd_d_out", "dec_bwd_w_2", "dec_bwd_d_2", "dec_bwd_w_1",
+                         "dec_bwd_d_z"})
+    c->bwd_dec_r.push_back(region(c, nm));
+  // ---- decoder on the lock rows
+  c->f_d1 = gd(B, c->d0, L + 1, c->z + (size_t)B * c->ldz, c->ldz, false, th + c->v1.off, c->d0,
+               false, c->a1, c->ld_d1, EPI_ACT);
+  c->f_d1.epi.act = act;
+  c->f_d2 = gd(B, c->d1, c->d0 + 1, c->a1, c->ld_d1, false, th + c->v2.off, c->d1, false, c->a2,
+               c->ld_d2, EPI_ACT);
+  c->f_d2.epi.act = act;
+  c->f_out = gd(B, c->D, c->d1 + 1, c->a2, c->ld_d2, false, th + c->vo.off, c->D, false, c->du,
+                c->ld_u, EPI_BCE);
+  c->f_out.epi.x = c->xs + (size_t)B * c->ldx;
+  c->f_out.epi.ldx = c->ldx;
+  c->f_out.epi.scale = c->inv_bg;
+  c->f_out.epi.rowpart = c->rowpart;
+  // ---- decoder backward (g1 only)
+  c->bwd_dec.clear();
+  c->bwd_dec.push_back(gd(c->d1 + 1, c->D, B, c->a2, c->ld_d2, true, c->du, c->ld_u, false,
+                          g1 + c->vo.off, c->D));
+  GemmDesc dout = gd(B, c->d1, c->D, c->du, c->ld_u, false, th + c->vo.off, c->D, true, c->dzd2,
+                     c->ld_d2, EPI_DACT);
+  dout.epi.act = act; dout.epi.aux = c->a2; dout.epi.ld_aux = c->ld_d2;
+  c->bwd_dec.push_back(dout);
+  c->bwd_dec.push_back(gd(c->d0 + 1, c->d1, B, c->a1, c->ld_d1, true, c->dzd2, c->ld_d2, false,
+                          g1 + c->v2.off, c->d1));
+  GemmDesc dd2 = gd(B, c->d0, c->d1, c->dzd2, c->ld_d2, false, th + c->v2.off, c->d1, true, c->dzd1,
+                    c->ld_d1, EPI_DACT);
+  dd2.epi.act = act; dd2.epi.aux = c->a1; dd2.epi.ld_aux = c->ld_d1;
+  c->bwd_dec.push_back(dd2);
+  c->bwd_dec.push_back(gd(L + 1, c->d0, B, c->z + (size_t)B * c->ldz, c->ldz, true, c->dzd1,
+                          c->ld_d1, false, g1 + c->v1.off, c->d0));
+  c->bwd_dec.push_back(gd(B, L, c->d0, c->dzd1, c->ld_d1, false, th + c->v1.off, c->d0, true,
+                          c->dzdec, L));
+  // ---- encoder backward: g1 over rows [rot|lock], g2 over [lock|key] (batched GEMMs)
+  c->bwd_enc.clear();
+  {
+    GemmDesc w = gd(c->head.K + 1, 2 * L, 2 * B, c->H[n - 1], c->ldh[n - 1], true, c->dhead, 2 * L,
+                    false, g1 + c->head.off, 2 * L);
+    w.batch = 2; w.sA = (long long)B * c->ldh[n - 1]; w.sB = (long long)2 * B * 2 * L; w.sC = n_all;
+    c->bwd_enc.push_back(w);
+    c->bwd_enc_r.push_back(region(c, "head_bwd_w"));
+    GemmDesc d = gd(4 * B, c->head.K, 2 * L, c->dhead, 2 * L, false, th + c->head.off, 2 * L, true,
+                    c->dz[(n - 1) & 1], c->lddz, EPI_DACT);
+    d.epi.act = act; d.epi.aux = c->H[n - 1]; d.epi.ld_aux = c->ldh[n - 1];
+    d.epi.remap_split = 2 * B; d.epi.remap_shift = B;
+    c->bwd_enc.push_back(d);
+    c->bwd_enc_r.push_back(region(c, "head_bwd_d"));
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    const float* A = i == 0 ? c->xs : c->H[i - 1];
+    const int lda = i == 0 ? c->ldx : c->ldh[i - 1];
+    GemmDesc w = gd(c->enc[i].K + 1, c->enc[i].N, 2 * B, A, lda, true, c->dz[i & 1], c->lddz, false,
+                    g1 + c->enc[i].off, c->enc[i].N);
+    w.batch = 2; w.sA = (long long)B * lda; w.sB = (long long)2 * B * c->lddz; w.sC = n_all;
+    c->bwd_enc.push_back(w);
+    c->bwd_enc_r.push_back(region(c, "enc_bwd_w_" + std::to_string(i)));
+    if (i > 0) {
+      GemmDesc d = gd(4 * B, c->enc[i].K, c->enc[i].N, c->dz[i & 1], c->lddz, false,
+                      th + c->enc[i].off, c->enc[i].N, true, c->dz[(i - 1) & 1], c->lddz, EPI_DACT);
+      d.epi.act = act; d.epi.aux = c->H[i - 1]; d.epi.ld_aux = c->ldh[i - 1];
+      d.epi.remap_split = 2 * B; d.epi.remap_shift = B;
+      c->bwd_enc.push_back(d);
+      c->bwd_enc_r.push_back(region(c, "enc_bwd_d_" + std::to_string(i)));
+    }
+  }
+  for (const char* nm : {"deinterleave", "eps_rng", "latent_fwd", "colsq", "metric_loss", "coldot",
+                         "latent_bwd", "adam"})
+    region(c, nm);
+}
+
+static int validate(const mvae_cfg* cfg) {
+  if (!cfg) return fail(nullptr, MVAE_EINVAL, "cfg is NULL");
+  if (cfg->image_size <= 0 || cfg->batch <= 0 || cfg->latent <= 0)
+    return fail(nullptr, MVAE_ECONFIG, "image_size, batch and latent must be positive");
+  if (cfg->global_batch < cfg->batch) return fail(nullptr, MVAE_ECONFIG, "global_batch < batch");
+  if (cfg->n_enc < 1 || cfg->n_enc > MVAE_MAX_ENC) return fail(nullptr, MVAE_ECONFIG, "n_enc out of range");
+  for (int i = 0; i < cfg->n_enc; ++i)
+    if (cfg->enc[i] <= 0) return fail(nullptr, MVAE_ECONFIG, "encoder width must be positive");
+  if (cfg->dec[0] <= 0 || cfg->dec[1] <= 0) return fail(nullptr, MVAE_ECONFIG, "decoder widths must be positive");
+  if (cfg->act != MVAE_ACT_TANH && cfg->act != MVAE_ACT_ELU) return fail(nullptr, MVAE_ECONFIG, "bad act");
+  if (cfg->metric != MVAE_METRIC_COSINE && cfg->metric != MVAE_METRIC_SQDIFF)
+    return fail(nullptr, MVAE_ECONFIG, "bad metric");
+  if (cfg->precision != MVAE_PREC_F32)
+    return fail(nullptr, MVAE_ECONFIG, "precision: only MVAE_PREC_F32 is built in this library");
+  const long long D = (long long)cfg->image_size * cfg->image_size;
+  if (D * 3 * cfg->batch > (1LL << 31) - 1 || 3LL * cfg->batch * (D + 4) > (1LL << 31) * 8)
+    return fail(nullptr, MVAE_ECONFIG, "batch too large for 32-bit row indexing");
+  return MVAE_OK;
+}
+
+extern "C" {
+
+int mvae_abi_version(void) { return MVAE_ABI_VERSION; }
+
+const char* mvae_last_error(mvae_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
+
+int mvae_destroy(mvae_ctx* ctx) {
+  if (!ctx) return MVAE_EINVAL;
+  int dev = 0;
+  hipGetDevice(&dev);
+  hipSetDevice(ctx->device);
+  hipDeviceSynchronize();
+  for (auto& pd : ctx->pending) { hipEventDestroy(pd.a); hipEventDestroy(pd.b); }
+  for (auto e : ctx->event_pool) hipEventDestroy(e);
+  for (void* p : ctx->allocs) hipFree(p);
+  hipSetDevice(dev);
+  delete ctx;
+  return MVAE_OK;
+}
+
+int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
+  if (!out) return fail(nullptr, MVAE_EINVAL, "out is NULL");
+  *out = nullptr;
+  int rc = validate(cfg);
+  if (rc) return rc;
+  mvae_ctx* ctx = new (std::nothrow) mvae_ctx();
+  if (!ctx) return fail(nullptr, MVAE_EINVAL, "out of host memory");
+  ctx->cfg = *cfg;
+  ctx->device = device;
+  hipError_t he = hipSetDevice(device);
+  if (he != hipSuccess) { g_create_err = hipGetErrorString(he); delete ctx; return (int)he; }
+  auto c = ctx;
+  c->B = cfg->batch;
+  c->D = cfg->image_size * cfg->image_size;
+  c->L = cfg->latent;
+  c->nenc = cfg->n_enc;
+  c->d0 = cfg->dec[0];
+  c->d1 = cfg->dec[1];
+  c->inv_bg = 1.f / (float)cfg->global_batch;
+  c->b1p[0] = c->b1p[1] = cfg->beta1;
+  c->b2p[0] = c->b2p[1] = cfg->beta2;
+  // ---- parameter layout
+  size_t off = 0;
+  int fan_in = c->D;
+  for (int i = 0; i < c->nenc; ++i) {
+    Block b; b.off = off; b.K = fan_in; b.N = cfg->enc[i];
+    c->enc.push_back(b);
+    off = align64(off + (size_t)(b.K + 1) * b.N);
+    fan_in = b.N;
+  }
+  c->head.off = off; c->head.K = fan_in; c->head.N = 2 * c->L;
+  off = align64(off + (size_t)(fan_in + 1) * 2 * c->L);
+  c->n_enc = off;
+  c->v1.off = off; c->v1.K = c->L; c->v1.N = c->d0;
+  off = align64(off + (size_t)(c->L + 1) * c->d0);
+  c->v2.off = off; c->v2.K = c->d0; c->v2.N = c->d1;
+  off = align64(off + (size_t)(c->d0 + 1) * c->d1);
+  c->vo.off = off; c->vo.K = c->d1; c->vo.N = c->D;
+  off = align64(off + (size_t)(c->d1 + 1) * c->D);
+  c->n_all = off;
+  // ---- strides
+  c->ldx = round4(c->D + 1);
+  c->ldz = round4(c->L + 1);
+  c->ld_d1 = round4(c->d0 + 1);
+  c->ld_d2 = round4(c->d1 + 1);
+  c->ld_u = round4(c->D);
+  int maxe = 0;
+  for (int i = 0; i < c->nenc; ++i) {
+    c->ldh.push_back(round4(cfg->enc[i] + 1));
+    maxe = std::max(maxe, cfg->enc[i]);
+  }
+  c->lddz = round4(maxe);
+  c->nblk = gemm_bce_nblk(c->D);
+  c->nchunk = colstats_nchunk(c->B);
+  const size_t B = c->B, L = c->L;
+#define ALLOC(p, n)                                              \
+  do {                                                           \
+    hipError_t e_ = dalloc(c, &(p), (n));                        \
+    if (e_ != hipSuccess) {                                      \
+      g_create_err = std::string("hipMalloc ") + #p + ": " + hipGetErrorString(e_); \
+      mvae_destroy(c);                                           \
+      return (int)e_;                                            \
+    }                                                            \
+  } while (0)
+  ALLOC(c->theta, c->n_all);
+  ALLOC(c->grads, c->n_all + c->n_enc);
+  ALLOC(c->adam, 2 * c->n_all + 2 * c->n_enc);
+  ALLOC(c->dead, (size_t)c->d1 * c->D + c->D);
+  ALLOC(c->xs, 3 * B * c->ldx);
+  c->H.resize(c->nenc);
+  for (int i = 0; i < c->nenc; ++i) ALLOC(c->H[i], 3 * B * c->ldh[i]);
+  ALLOC(c->ms, 3 * B * 2 * L);
+  ALLOC(c->z, 3 * B * c->ldz);
+  ALLOC(c->zgen, B * c->ldz);
+  ALLOC(c->a1, B * c->ld_d1);
+  ALLOC(c->a2, B * c->ld_d2);
+  ALLOC(c->du, B * c->ld_u);
+  ALLOC(c->rowpart, B * c->nblk);
+  ALLOC(c->rowvals, 4 * B);
+  ALLOC(c->dist, B);
+  ALLOC(c->draw, B);
+  ALLOC(c->losses, 8);
+  ALLOC(c->colsq, 2 * L);
+  ALLOC(c->coldot, L);
+  ALLOC(c->cspart, (size_t)c->nchunk * 2 * L);
+  ALLOC(c->eps, 3 * B * L);
+  ALLOC(c->dzd2, B * c->ld_d2);
+  ALLOC(c->dzd1, B * c->ld_d1);
+  ALLOC(c->dzdec, B * L);
+  ALLOC(c->dhead, 4 * B * 2 * L);
+  ALLOC(c->dz[0], 4 * B * c->lddz);
+  ALLOC(c->dz[1], 4 * B * c->lddz);
+  // constant ones columns (bias folding)
+  hipError_t e = ones_column(c->xs, c->ldx, c->D, 3 * (int)B);
+  for (int i = 0; e == hipSuccess && i < c->nenc; ++i) e = ones_column(c->H[i], c->ldh[i], cfg->enc[i], 3 * (int)B);
+  if (e == hipSuccess) e = ones_column(c->z, c->ldz, c->L, 3 * (int)B);
+  if (e == hipSuccess) e = ones_column(c->zgen, c->ldz, c->L, (int)B);
+  if (e == hipSuccess) e = ones_column(c->a1, c->ld_d1, c->d0, (int)B);
+  if (e == hipSuccess) e = ones_column(c->a2, c->ld_d2, c->d1, (int)B);
+  if (e != hipSuccess) {
+    g_create_err = std::string("ones column: ") + hipGetErrorString(e);
+    mvae_destroy(c);
+    return (int)e;
+  }
+  build_schedule(c);
+  size_t ws = 0;
+  for (auto& d : c->fwd_enc) ws = std::max(ws, gemm_workspace_elems(d));
+  for (auto& d : c->bwd_dec) ws = std::max(ws, gemm_workspace_elems(d));
+  for (auto& d : c->bwd_enc) ws = std::max(ws, gemm_workspace_elems(d));
+  ws = std::max(ws, gemm_workspace_elems(c->f_d1));
+  ws = std::max(ws, gemm_workspace_elems(c->f_d2));
+  c->ws_elems = ws;
+  ALLOC(c->ws, ws);
+#undef ALLOC
+  *out = c;
+  return MVAE_OK;
+}
+
+int mvae_param_count(mvae_ctx* ctx) { return ctx ? 2 * ctx->nenc + 4 + 8 : MVAE_EINVAL; }
+
+int mvae_param_info(mvae_ctx* ctx, int kind, int index, mvae_tensor* out) {
+  if (!ctx || !out) return MVAE_EINVAL;
+  const int n = ctx->nenc;
+  const int count = mvae_param_count(ctx);
+  if (index < 0 || index >= count) return fail(ctx, MVAE_EINVAL, "param index out of range");
+  std::memset(out, 0, sizeof(*out));
+  // resolve (name, block-relative pointer) in reference creation order (11a/vae.py:85-153)
+  const Block* blk = nullptr;
+  bool bias = false;
+  int col0 = 0, cols = 0, ld = 0, enc_part = 0;
+  std::string name;
+  if (index < 2 * n) {
+    const int i = index / 2;
+    bias = index & 1;
+    blk = &ctx->enc[i];
+    name = "enc_h" + std::to_string(i) + (bias ? "_b" : "_W");
+    cols = blk->N; ld = blk->N; enc_part = 1;
+  } else if (index < 2 * n + 4) {
+    const int j = index - 2 * n;
+    blk = &ctx->head;
+    bias = j & 1;
+    const bool logsig = j >= 2;
+    name = std::string(logsig ? "enc_out_log_sigma" : "enc_out_mean") + (bias ? "_b" : "_W");
+    col0 = logsig ? ctx->L : 0; cols = ctx->L; ld = 2 * ctx->L; enc_part = 1;
+  } else if (index < 2 * n + 10) {
+    const int j = index - 2 * n - 4;
+    const Block* bl[3] = {&ctx->v1, &ctx->v2, &ctx->vo};
+    const char* nm[3] = {"dec_h1", "dec_h2", "dec_out_mean"};
+    blk = bl[j / 2];
+    bias = j & 1;
+    name = std::string(nm[j / 2]) + (bias ? "_b" : "_W");
+    cols = blk->N; ld = blk->N;
+  } else {  // dead decoder log-sigma variables (11a/vae.py:147,153): allocated, never trained
+    bias = (index - 2 * n - 10) == 1;
+    std::strncpy(out->name, bias ? "dec_out_log_sigma_b" : "dec_out_log_sigma_W", sizeof(out->name) - 1);
+    if (kind != MVAE_KIND_PARAM) return fail(ctx, MVAE_EINVAL, "dead variables have no optimizer state");
+    out->data = ctx->dead + (bias ? (size_t)ctx->d1 * ctx->D : 0);
+    out->rows = bias ? 1 : ctx->d1;
+    out->cols = ctx->D;
+    out->ld = ctx->D;
+    out->trained_by = 0;
+    return MVAE_OK;
+  }
+  std::strncpy(out->name, name.c_str(), sizeof(out->name) - 1);
+  float* base = nullptr;
+  switch (kind) {
+    case MVAE_KIND_PARAM: base = ctx->theta; break;
+    case MVAE_KIND_GRAD1: base = ctx->grads; break;
+    case MVAE_KIND_GRAD2: base = enc_part ? ctx->grads + ctx->n_all : nullptr; break;
+    case MVAE_KIND_M1: base = ctx->adam; break;
+    case MVAE_KIND_V1: base = ctx->adam + ctx->n_all; break;
+    case MVAE_KIND_M2: base = enc_part ? ctx->adam + 2 * ctx->n_all : nullptr; break;
+    case MVAE_KIND_V2: base = enc_part ? ctx->adam + 2 * ctx->n_all + ctx->n_enc : nullptr; break;
+    default: return fail(ctx, MVAE_EINVAL, "bad kind");
+  }
+  if (!base) return fail(ctx, MVAE_EINVAL, "decoder variables are not trained by the metric optimizer");
+  out->data = base + blk->off + (bias ? (size_t)blk->K * ld : 0) + col0;
+  out->rows = bias ? 1 : blk->K;
+  out->cols = cols;
+  out->ld = ld;
+  out->trained_by = enc_part ? 3 : 1;
+  return MVAE_OK;
+}
+
+int mvae_buffer(mvae_ctx* ctx, int which, float** ptr, size_t* count) {
+  if (!ctx || !ptr || !count) return MVAE_EINVAL;
+  switch (which) {
+    case MVAE_BUF_PARAMS: *ptr = ctx->theta; *count = ctx->n_all; break;
+    case MVAE_BUF_GRADS: *ptr = ctx->grads; *count = ctx->n_all + ctx->n_enc; break;
+    case MVAE_BUF_ADAM: *ptr = ctx->adam; *count = 2 * ctx->n_all + 2 * ctx->n_enc; break;
+    case MVAE_BUF_LOSSES: *ptr = ctx->losses; *count = 5; break;
+    case MVAE_BUF_COLSQ: *ptr = ctx->colsq; *count = 2 * (size_t)ctx->L; break;
+    case MVAE_BUF_COLDOT: *ptr = ctx->coldot; *count = ctx->L; break;
+    case MVAE_BUF_DIST: *ptr = ctx->dist; *count = ctx->B; break;
+    case MVAE_BUF_GRADS_DEC: *ptr = ctx->grads + ctx->n_enc; *count = ctx->n_all - ctx->n_enc; break;
+    case MVAE_BUF_DEAD: *ptr = ctx->dead; *count = (size_t)ctx->d1 * ctx->D + ctx->D; break;
+    case MVAE_BUF_EPS: *ptr = ctx->eps; *count = (size_t)3 * ctx->B * ctx->L; break;
+    default: return fail(ctx, MVAE_EINVAL, "bad buffer id");
+  }
+  return MVAE_OK;
+}
+
+int mvae_get_step(mvae_ctx* ctx, int64_t* t1, int64_t* t2) {
+  if (!ctx || !t1 || !t2) return MVAE_EINVAL;
+  *t1 = ctx->t1; *t2 = ctx->t2;
+  return MVAE_OK;
+}
+
+int mvae_set_step(mvae_ctx* ctx, int64_t t1, int64_t t2) {
+  if (!ctx || t1 < 0 || t2 < 0) return MVAE_EINVAL;
+  ctx->t1 = t1; ctx->t2 = t2;
+  // recompute the fp32 beta powers exactly as TF accumulates them (one fp32 multiply per step)
+  for (int o = 0; o < 2; ++o) {
+    const int64_t t = o == 0 ? t1 : t2;
+    float b1p = ctx->cfg.beta1, b2p = ctx->cfg.beta2;
+    for (int64_t s = 0; s < t; ++s) { b1p *= ctx->cfg.beta1; b2p *= ctx->cfg.beta2; }
+    ctx->b1p[o] = b1p; ctx->b2p[o] = b2p;
+  }
+  return MVAE_OK;
+}
+
+int mvae_sync_params(mvae_ctx* ctx, void* stream) {
+  (void)stream;
+  return ctx ? MVAE_OK : MVAE_EINVAL;  // fp32 build: no shadows to refresh
+}
+
+// ------------------------------------------------------------------ phases
+static int run(mvae_ctx* ctx, const GemmDesc& d, hipStream_t st, int r = -1) {
+  TimeScope ts(ctx, r < 0 ? region(ctx, "other_gemm") : r, st);
+  MV_CHECK(gemm_run(d, ctx->ws, ctx->ws_elems, st));
+  return MVAE_OK;
+}
+#define TIMED(name) TimeScope ts_##__LINE__(ctx, region(ctx, name), st)
+
+static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t st) {
+  auto c = ctx;
+  {
+    TIMED("deinterleave");
+    MV_CHECK(launch_deinterleave(x, c->xs, nullptr, c->B, c->D, c->ldx, st));
+  }
+  const size_t ne = (size_t)3 * c->B * c->L;
+  {
+    TIMED("eps_rng");
+    if (eps) {
+      MV_CHECK(hipMemcpyAsync(c->eps, eps, ne * sizeof(float), hipMemcpyDeviceToDevice, st));
+    } else {
+      MV_CHECK(launch_normal(c->eps, ne, c->cfg.seed, c->rng_counter++, st));
+    }
+  }
+  for (size_t i = 0; i < c->fwd_enc.size(); ++i) {
+    int rc = run(c, c->fwd_enc[i], st, c->fwd_enc_r[i]);
+    if (rc) return rc;
+  }
+  {
+    TIMED("latent_fwd");
+    MV_CHECK(launch_latent_fwd(c->ms, c->eps, c->z, nullptr, c->B, c->L, c->ldz, st));
+  }
+  if (c->cfg.metric == MVAE_METRIC_COSINE) {
+    TIMED("colsq");
+    MV_CHECK(launch_colstats(0, c->z, c->B, c->L, c->ldz, nullptr, nullptr, c->cspart, c->nchunk,
+                             c->colsq, st));
+  }
+  return MVAE_OK;
+}
+
+extern "C" int mvae_forward(mvae_ctx* ctx, const float* x, const float* eps, void* stream) {
+  if (!ctx || !x) return MVAE_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  int rc = encode(ctx, x, eps, st);
+  if (rc) return rc;
+  if ((rc = run(ctx, ctx->f_d1, st, ctx->f_d1_r))) return rc;
+  if ((rc = run(ctx, ctx->f_d2, st, ctx->f_d2_r))) return rc;
+  if ((rc = run(ctx, ctx->f_out, st, ctx->f_out_r))) return rc;
+  ctx->phase = 1;
+  return MVAE_OK;
+}
+
+extern "C" int mvae_metric(mvae_ctx* ctx, const float* areas, void* stream) {
+  if (!ctx || !areas) return MVAE_EINVAL;
+  if (ctx->phase != 1) return fail(ctx, MVAE_ESTATE, "mvae_metric before mvae_forward");
+  hipStream_t st = (hipStream_t)stream;
+  auto c = ctx;
+  {
+    TIMED("metric_loss");
+    MV_CHECK(launch_metric(c->z, c->ldz, c->ms, c->rowpart, c->nblk, areas, c->colsq, c->B, c->L,
+                           c->cfg.metric, c->cfg.reciprocal, c->cfg.deform_weight, c->inv_bg,
+                           c->rowvals, c->dist, c->draw, st));
+    MV_CHECK(launch_loss_reduce(c->rowvals, c->B, c->inv_bg, c->losses, st));
+  }
+  if (c->cfg.metric == MVAE_METRIC_COSINE) {
+    TIMED("coldot");
+    MV_CHECK(launch_colstats(1, c->z, c->B, c->L, c->ldz, c->colsq, c->draw, c->cspart, c->nchunk,
+                             c->coldot, st));
+  }
+  ctx->phase = 2;
+  return MVAE_OK;
+}
+
+extern "C" int mvae_backward(mvae_ctx* ctx, void* stream) {
+  if (!ctx) return MVAE_EINVAL;
+  if (ctx->phase != 2) return fail(ctx, MVAE_ESTATE, "mvae_backward before mvae_metric");
+  hipStream_t st = (hipStream_t)stream;
+  auto c = ctx;
+  int rc;
+  for (size_t i = 0; i < c->bwd_dec.size(); ++i)
+    if ((rc = run(c, c->bwd_dec[i], st, c->bwd_dec_r[i]))) return rc;
+  {
+    TIMED("latent_bwd");
+    MV_CHECK(launch_latent_bwd(c->z, c->ldz, c->ms, c->eps, c->dzdec, c->draw, c->colsq, c->coldot,
+                               c->B, c->L, c->cfg.metric, c->cfg.deform_weight, c->inv_bg, c->dhead,
+                               nullptr, st));
+  }
+  for (size_t i = 0; i < c->bwd_enc.size(); ++i)
+    if ((rc = run(c, c->bwd_enc[i], st, c->bwd_enc_r[i]))) return rc;
+  ctx->phase = 3;
+  return MVAE_OK;
+}
+
+extern "C" int mvae_adam(mvae_ctx* ctx, void* stream) {
+  if (!ctx) return MVAE_EINVAL;
+  if (ctx->phase != 3) return fail(ctx, MVAE_ESTATE, "mvae_adam before mvae_backward");
+  auto c = ctx;
+  AdamArgs a;
+  a.theta = c->theta; a.g1 = c->grads; a.g2 = c->grads + c->n_all;
+  a.m1 = c->adam; a.v1 = c->adam + c->n_all;
+  a.m2 = c->adam + 2 * c->n_all; a.v2 = c->adam + 2 * c->n_all + c->n_enc;
+  a.n_all = c->n_all; a.n_enc = c->n_enc;
+  a.b1 = c->cfg.beta1; a.b2 = c->cfg.beta2; a.eps = c->cfg.epsilon;
+  // TF ApplyAdam: lr_t = lr * sqrt(1 - beta2_power) / (1 - beta1_power), all fp32
+  a.lr1 = (c->cfg.lr[0] * std::sqrt(1.f - c->b2p[0])) / (1.f - c->b1p[0]);
+  a.lr2 = (c->cfg.lr[1] * std::sqrt(1.f - c->b2p[1])) / (1.f - c->b1p[1]);
+  a.theta_h = nullptr;
+  hipStream_t st = (hipStream_t)stream;
+  {
+    TIMED("adam");
+    MV_CHECK(launch_adam(a, st));
+  }
+  for (int o = 0; o < 2; ++o) { c->b1p[o] *= c->cfg.beta1; c->b2p[o] *= c->cfg.beta2; }
+  c->t1++; c->t2++;
+  ctx->phase = 0;
+  return MVAE_OK;
+}
+
+extern "C" int mvae_train_step(mvae_ctx* ctx, const float* x, const float* areas, const float* eps,
+                               float* losses_out, float* dist_out, void* stream) {
+  if (!ctx || !x || !areas) return MVAE_EINVAL;
+  int rc;
+  if ((rc = mvae_forward(ctx, x, eps, stream))) return rc;
+  if ((rc = mvae_metric(ctx, areas, stream))) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  if (losses_out) MV_CHECK(hipMemcpyAsync(losses_out, ctx->losses, 5 * sizeof(float), hipMemcpyDeviceToDevice, st));
+  if (dist_out) MV_CHECK(hipMemcpyAsync(dist_out, ctx->dist, ctx->B * sizeof(float), hipMemcpyDeviceToDevice, st));
+  if ((rc = mvae_backward(ctx, stream))) return rc;
+  return mvae_adam(ctx, stream);
+}
+
+extern "C" int mvae_predict(mvae_ctx* ctx, const float* x, const float* eps, float* dist_out, void* stream) {
+  if (!ctx || !x || !dist_out) return MVAE_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  int rc = encode(ctx, x, eps, st);
+  if (rc) return rc;
+  auto c = ctx;
+  MV_CHECK(launch_metric(c->z, c->ldz, c->ms, c->rowpart, c->nblk, nullptr, c->colsq, c->B, c->L,
+                         c->cfg.metric, c->cfg.reciprocal, c->cfg.deform_weight, c->inv_bg,
+                         c->rowvals, dist_out, c->draw, st));
+  ctx->phase = 0;
+  return MVAE_OK;
+}
+
+extern "C" int mvae_transform(mvae_ctx* ctx, const float* x, float* zmean_out, void* stream) {
+  if (!ctx || !x || !zmean_out) return MVAE_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  int rc = encode(ctx, x, nullptr, st);
+  if (rc) return rc;
+  MV_CHECK(launch_copy2d(ctx->ms + (size_t)ctx->B * 2 * ctx->L, 2 * ctx->L, zmean_out, ctx->L,
+                         ctx->B, ctx->L, st));
+  ctx->phase = 0;
+  return MVAE_OK;
+}
+
+extern "C" int mvae_reconstruct(mvae_ctx* ctx, const float* x, const float* eps, float* y_out, void* stream) {
+  if (!ctx || !x || !y_out) return MVAE_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  int rc = encode(ctx, x, eps, st);
+  if (rc) return rc;
+  if ((rc = run(ctx, ctx->f_d1, st))) return rc;
+  if ((rc = run(ctx, ctx->f_d2, st))) return rc;
+  GemmDesc d = ctx->f_out;
+  d.epi.y = y_out;
+  d.epi.ldy = ctx->D;
+  if ((rc = run(ctx, d, st))) return rc;
+  ctx->phase = 0;
+  return MVAE_OK;
+}
+
+extern "C" int mvae_generate(mvae_ctx* ctx, const float* zin, int n, float* y_out, void* stream) {
+  if (!ctx || !zin || !y_out || n <= 0 || n > ctx->B) return MVAE_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  auto c = ctx;
+  MV_CHECK(launch_copy2d(zin, c->L, c->zgen, c->ldz, n, c->L, st));
+  GemmDesc d1 = c->f_d1; d1.M = n; d1.A = c->zgen;
+  GemmDesc d2 = c->f_d2; d2.M = n;
+  GemmDesc d3 = gd(n, c->D, c->d1 + 1, c->a2, c->ld_d2, false, c->theta + c->vo.off, c->D, false,
+                   y_out, c->D, EPI_SIGMOID);
+  int rc;
+  if ((rc = run(c, d1, st))) return rc;
+  if ((rc = run(c, d2, st))) return rc;
+  if ((rc = run(c, d3, st))) return rc;
+  ctx->phase = 0;
+  return MVAE_OK;
+}
+
+}  // extern "C"
+
+extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int at, const float* Bm,
+                               int ldb, int bt, float* Cm, int ldc, int epi, int act, const float* aux,
+                               int ld_aux, void* stream) {
+  if (epi == EPI_BCE || epi < 0 || epi > EPI_SIGMOID) return fail(nullptr, MVAE_EINVAL, "bad epilogue");
+  GemmDesc d = gd(M, N, K, A, lda, at != 0, Bm, ldb, bt != 0, Cm, ldc, epi);
+  d.epi.act = act;
+  d.epi.aux = aux;
+  d.epi.ld_aux = ld_aux;
+  const size_t ws_n = gemm_workspace_elems(d);
+  float* ws = nullptr;
+  if (ws_n && hipMalloc(&ws, ws_n * sizeof(float)) != hipSuccess) return fail(nullptr, MVAE_EINVAL, "ws alloc");
+  hipError_t e = gemm_run(d, ws, ws_n, (hipStream_t)stream);
+  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+  if (ws) (void)hipFree(ws);
+  if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
+  return MVAE_OK;
+}
+
+extern "C" int mvae_timing_enable(mvae_ctx* ctx, int on) {
+  if (!ctx) return MVAE_EINVAL;
+  ctx->timing = on != 0;
+  return MVAE_OK;
+}
+
+extern "C" int mvae_timing_regions(mvae_ctx* ctx) {
+  return ctx ? (int)ctx->region_names.size() : MVAE_EINVAL;
+}
+
+extern "C" const char* mvae_timing_name(mvae_ctx* ctx, int r) {
+  if (!ctx || r < 0 || r >= (int)ctx->region_names.size()) return nullptr;
+  return ctx->region_names[r].c_str();
+}
+
+static int collect(mvae_ctx* ctx) {
+  for (auto& pd : ctx->pending) {
+    MV_CHECK(hipEventSynchronize(pd.b));
+    float ms = 0.f;
+    MV_CHECK(hipEventElapsedTime(&ms, pd.a, pd.b));
+    ctx->region_ms[pd.region] += ms;
+    ctx->region_n[pd.region] += 1;
+    ctx->event_pool.push_back(pd.a);
+    ctx->event_pool.push_back(pd.b);
+  }
+  ctx->pending.clear();
+  return MVAE_OK;
+}
+
+extern "C" int mvae_timing_read(mvae_ctx* ctx, int r, double* total_ms, int64_t* count) {
+  if (!ctx || !total_ms || !count || r < 0 || r >= (int)ctx->region_names.size()) return MVAE_EINVAL;
+  int rc = collect(ctx);
+  if (rc) return rc;
+  *total_ms = ctx->region_ms[r];
+  *count = ctx->region_n[r];
+  return MVAE_OK;
+}
+
+extern "C" int mvae_timing_reset(mvae_ctx* ctx) {
+  if (!ctx) return MVAE_EINVAL;
+  int rc = collect(ctx);
+  if (rc) return rc;
+  std::fill(ctx->region_ms.begin(), ctx->region_ms.end(), 0.0);
+  std::fill(ctx->region_n.begin(), ctx->region_n.end(), 0);
+  return MVAE_OK;
+}

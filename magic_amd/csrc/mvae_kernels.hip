@@ -1,0 +1,429 @@
+// Bandwidth-bound kernels of the metric-VAE step (gfx950): batch de-interleave, the
+// counter-based N(0,1) sampler, reparameterisation, the latent loss head forward/backward
+// (KL, deformation, cosine / squared-difference distance, training_loss), deterministic
+// loss/column reductions, and the fused dual TF-Adam update.
+//
+// Row order of every stacked encoder buffer: [rotated lock | lock | key] (3B rows), so the
+// cost gradient (rotated+lock) and the metric gradient (lock+key) each use a CONTIGUOUS
+// 2B-row range. The backward stacks 4B rows: [rot(g1) | lock(g1) | lock(g2) | key(g2)].
+#include "mvae_internal.h"
+
+namespace mvae {
+namespace {
+
+constexpr float L2_EPS = 1e-12f;  // tf.nn.l2_normalize default
+
+// internal block (0 rot, 1 lock, 2 key) -> reference eps slot (0 lock, 1 rot, 2 key)
+__device__ __forceinline__ int eps_slot(int blk) { return blk == 0 ? 1 : (blk == 1 ? 0 : 2); }
+
+// ---------------------------------------------------------------- de-interleave
+// x[b][p*3 + c] (c: 0 lock, 1 rotated lock, 2 key; 11a/overlap_input.py:117-119,201)
+//  -> xs[(blk*B + b)][p], blk = {rot:0, lock:1, key:2}. Each thread moves 4 pixels:
+// three 16-B loads, three 16-B stores (coalesced both ways).
+__global__ void deinterleave_vec_kernel(const float4* __restrict__ x, float* __restrict__ xs,
+                                        __hip_bfloat16* __restrict__ xsh, int B, int D, int ldx) {
+  const int b = blockIdx.y;
+  const int q = blockIdx.x * blockDim.x + threadIdx.x;  // pixel quad
+  if (q * 4 >= D) return;
+  const float4* src = x + ((size_t)b * 3 * D) / 4 + 3 * q;
+  const float4 v0 = src[0], v1 = src[1], v2 = src[2];
+  // pixels p0..p3: (l,r,k) = (v0.x v0.y v0.z) (v0.w v1.x v1.y) (v1.z v1.w v2.x) (v2.y v2.z v2.w)
+  const float4 lock = make_float4(v0.x, v0.w, v1.z, v2.y);
+  const float4 rot = make_float4(v0.y, v1.x, v1.w, v2.z);
+  const float4 key = make_float4(v0.z, v1.y, v2.x, v2.w);
+  const size_t col = 4 * (size_t)q;
+  *reinterpret_cast<float4*>(xs + (size_t)b * ldx + col) = rot;
+  *reinterpret_cast<float4*>(xs + (size_t)(B + b) * ldx + col) = lock;
+  *reinterpret_cast<float4*>(xs + (size_t)(2 * B + b) * ldx + col) = key;
+  if (xsh) {
+    const float4 vv[3] = {rot, lock, key};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      __hip_bfloat16* d = xsh + (size_t)(c * B + b) * ldx + col;
+      d[0] = __float2bfloat16(vv[c].x); d[1] = __float2bfloat16(vv[c].y);
+      d[2] = __float2bfloat16(vv[c].z); d[3] = __float2bfloat16(vv[c].w);
+    }
+  }
+}
+
+__global__ void deinterleave_scalar_kernel(const float* __restrict__ x, float* __restrict__ xs,
+                                           __hip_bfloat16* __restrict__ xsh, int B, int D, int ldx) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= D) return;
+  const float* src = x + (size_t)b * 3 * D + 3 * (size_t)p;
+  const float v[3] = {src[1], src[0], src[2]};  // rot, lock, key
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    xs[(size_t)(c * B + b) * ldx + p] = v[c];
+    if (xsh) xsh[(size_t)(c * B + b) * ldx + p] = __float2bfloat16(v[c]);
+  }
+}
+
+// ---------------------------------------------------------------- N(0,1) sampler
+// Philox4x32-10 counter-based generator + Box-Muller; element i of call `counter` depends
+// only on (seed, counter, i): reproducible and independent of the launch geometry.
+__device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    const uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0;
+    const uint32_t h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+    const uint32_t n0 = h1 ^ c[1] ^ k0, n2 = h0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = l1; c[2] = n2; c[3] = l0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+
+__global__ void normal_kernel(float* __restrict__ out, size_t n, uint64_t seed, uint64_t counter) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // one Philox block -> 4 normals
+  if (4 * i >= n) return;
+  uint32_t c[4] = {(uint32_t)i, (uint32_t)(i >> 32), (uint32_t)counter, (uint32_t)(counter >> 32)};
+  philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float inv = 2.3283064365386963e-10f;  // 2^-32
+  float r[4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float u1 = ((float)c[2 * j] + 0.5f) * inv;  // (0,1)
+    const float u2 = ((float)c[2 * j + 1] + 0.5f) * inv;
+    const float rad = sqrtf(-2.f * logf(u1));
+    float s, co;
+    sincosf(6.283185307179586f * u2, &s, &co);
+    r[2 * j] = rad * co;
+    r[2 * j + 1] = rad * s;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (4 * i + j < n) out[4 * i + j] = r[j];
+}
+
+// ---------------------------------------------------------------- reparameterisation
+// z = mu + sqrt(exp(s)) * eps   (11a/vae.py:371-377); ms rows = [mu | s] (2L wide)
+__global__ void latent_fwd_kernel(const float* __restrict__ ms, const float* __restrict__ eps,
+                                  float* __restrict__ z, __hip_bfloat16* __restrict__ zh, int B,
+                                  int L, int ldz) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)3 * B * L) return;
+  const int r = (int)(idx / L), i = (int)(idx - (size_t)r * L);
+  const int blk = r / B, b = r - blk * B;
+  const float mu = ms[(size_t)r * 2 * L + i];
+  const float s = ms[(size_t)r * 2 * L + L + i];
+  const float e = eps[((size_t)eps_slot(blk) * B + b) * L + i];
+  const float v = mu + sqrtf(expf(s)) * e;
+  z[(size_t)r * ldz + i] = v;
+  if (zh) zh[(size_t)r * ldz + i] = __float2bfloat16(v);
+}
+
+// ---------------------------------------------------------------- column statistics
+// mode 0 (colsq):  out[j] = sum_b z_lock[b][j]^2 (j < L), sum_b z_key[b][j-L]^2 (j >= L)
+// mode 1 (coldot): out[i] = sum_b draw_b * n_lock[b][i] * n_key[b][i]
+// Two-stage, fixed-order (deterministic): partials over row chunks, then chunk sums.
+constexpr int CS_ROWS = 128;
+__global__ void colstats_part_kernel(int mode, const float* __restrict__ z, int B, int L, int ldz,
+                                     const float* __restrict__ colsq, const float* __restrict__ draw,
+                                     float* __restrict__ part) {
+  const int ncols = mode == 0 ? 2 * L : L;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 cols x 4 row lanes
+  const int j = blockIdx.x * 64 + tx;
+  const int r0 = blockIdx.y * CS_ROWS;
+  const int r1 = min(B, r0 + CS_ROWS);
+  __shared__ float red[4][64];
+  float acc = 0.f;
+  if (j < ncols) {
+    if (mode == 0) {
+      const float* src = j < L ? z + (size_t)B * ldz + j : z + (size_t)2 * B * ldz + (j - L);
+      for (int b = r0 + ty; b < r1; b += 4) {
+        const float v = src[(size_t)b * ldz];
+        acc += v * v;
+      }
+    } else {
+      const float rl = rsqrtf(fmaxf(colsq[j], L2_EPS));
+      const float rk = rsqrtf(fmaxf(colsq[L + j], L2_EPS));
+      for (int b = r0 + ty; b < r1; b += 4) {
+        const float zl = z[(size_t)(B + b) * ldz + j], zk = z[(size_t)(2 * B + b) * ldz + j];
+        acc += draw[b] * (zl * rl) * (zk * rk);
+      }
+    }
+  }
+  red[ty][tx] = acc;
+  __syncthreads();
+  if (ty == 0 && j < ncols)
+    part[(size_t)blockIdx.y * ncols + j] = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
+}
+
+__global__ void colstats_final_kernel(const float* __restrict__ part, int nchunk, int ncols,
+                                      float* __restrict__ out) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= ncols) return;
+  float acc = 0.f;
+  for (int c = 0; c < nchunk; ++c) acc += part[(size_t)c * ncols + j];
+  out[j] = acc;
+}
+
+// ---------------------------------------------------------------- metric / losses per row
+// One wave per batch row b. rowvals[b] = {R_b, K_b, F_b, T_b}; dist[b]; draw[b] = dT/draw_b.
+//   R_b: BCE row partials from the decoder-output GEMM epilogue (11a/vae.py:266-269)
+//   K_b = -0.5 sum(1 + s - mu^2 - exp(s))            (lock pass, :281-284)
+//   F_b = w sum (z_lock - z_rot)^2                    (:293-294)
+//   dist_b: cosine (axis-0 l2_normalize, :444-458) or sum (z_lock - z_key)^2; 1/raw if recip
+//   T_b = (dist_b - area_b)^2                         (:313)
+__global__ void metric_kernel(const float* __restrict__ z, int ldz, const float* __restrict__ ms,
+                              const float* __restrict__ rowpart, int nblk,
+                              const float* __restrict__ areas, const float* __restrict__ colsq,
+                              int B, int L, int metric, int recip, float w, float inv_bg,
+                              float* __restrict__ rowvals, float* __restrict__ dist,
+                              float* __restrict__ draw) {
+  const int lane = threadIdx.x & 63;
+  const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (b >= B) return;
+  const float* zr = z + (size_t)b * ldz;
+  const float* zl = z + (size_t)(B + b) * ldz;
+  const float* zk = z + (size_t)(2 * B + b) * ldz;
+  const float* msl = ms + (size_t)(B + b) * 2 * L;
+  float kl = 0.f, fd = 0.f, raw = 0.f, rp = 0.f;
+  for (int i = lane; i < L; i += 64) {
+    const float mu = msl[i], s = msl[L + i];
+    kl += 1.f + s - mu * mu - expf(s);
+    const float d = zl[i] - zr[i];
+    fd += d * d;
+    if (metric == 0) {
+      const float rl = rsqrtf(fmaxf(colsq[i], L2_EPS));
+      const float rk = rsqrtf(fmaxf(colsq[L + i], L2_EPS));
+      raw += (zl[i] * rl) * (zk[i] * rk);
+    } else {
+      const float e = zl[i] - zk[i];
+      raw += e * e;
+    }
+  }
+  for (int j = lane; j < nblk; j += 64) rp += rowpart[(size_t)b * nblk + j];
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    kl += __shfl_xor(kl, off, 64);
+    fd += __shfl_xor(fd, off, 64);
+    raw += __shfl_xor(raw, off, 64);
+    rp += __shfl_xor(rp, off, 64);
+  }
+  if (lane == 0) {
+    const float dv = recip ? 1.f / raw : raw;
+    const float a = areas ? areas[b] : 0.f;
+    const float g = 2.f * (dv - a) * inv_bg;
+    rowvals[4 * (size_t)b + 0] = rp;
+    rowvals[4 * (size_t)b + 1] = -0.5f * kl;
+    rowvals[4 * (size_t)b + 2] = w * fd;
+    rowvals[4 * (size_t)b + 3] = (dv - a) * (dv - a);
+    dist[b] = dv;
+    draw[b] = recip ? -g * dv * dv : g;  // tf.reciprocal grad: -dy * y^2
+  }
+}
+
+// single block, fixed-order: losses = {cost, training_loss, r_l, l_l, d_l} (local sums / B_global)
+__global__ void loss_reduce_kernel(const float* __restrict__ rowvals, int B, float inv_bg,
+                                   float* __restrict__ losses) {
+  __shared__ float red[4][256];
+  float a[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int b = threadIdx.x; b < B; b += 256) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[q] += rowvals[4 * (size_t)b + q];
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) red[q][threadIdx.x] = a[q];
+  __syncthreads();
+  for (int s = 128; s >= 1; s >>= 1) {
+    if ((int)threadIdx.x < s) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const float R = red[0][0] * inv_bg, K = red[1][0] * inv_bg, F = red[2][0] * inv_bg;
+    losses[0] = R + K + F;
+    losses[1] = red[3][0] * inv_bg;
+    losses[2] = R;
+    losses[3] = K;
+    losses[4] = F;
+  }
+}
+
+// ---------------------------------------------------------------- latent head backward
+// dhead rows (4B): [rot:g1 | lock:g1 | lock:g2 | key:g2], cols [dmu (L) | ds (L)]
+//   g1: dz_rot = -2w(zl-zr)/B ; dz_lock = dz_dec + 2w(zl-zr)/B, + KL: dmu += mu/B,
+//       ds += 0.5(exp(s)-1)/B
+//   g2: sqdiff: dz_lock = 2 draw (zl-zk) = -dz_key
+//       cosine: dz = r (draw n_other - n c), c = coldot (summed over the global batch),
+//               the n*c term only where sum z^2 >= 1e-12 (tf.maximum routes the gradient)
+//   reparameterisation: dmu = dz, ds = 0.5 dz eps sigma
+__global__ void latent_bwd_kernel(const float* __restrict__ z, int ldz, const float* __restrict__ ms,
+                                  const float* __restrict__ eps, const float* __restrict__ dzdec,
+                                  const float* __restrict__ draw, const float* __restrict__ colsq,
+                                  const float* __restrict__ coldot, int B, int L, int metric,
+                                  float w, float inv_bg, float* __restrict__ dhead,
+                                  __hip_bfloat16* __restrict__ dheadh) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)4 * B * L) return;
+  const int r = (int)(idx / L), i = (int)(idx - (size_t)r * L);
+  const int q = r / B, b = r - q * B;
+  const float zr = z[(size_t)b * ldz + i];
+  const float zl = z[(size_t)(B + b) * ldz + i];
+  const float zk = z[(size_t)(2 * B + b) * ldz + i];
+  const int fwd_blk = q == 0 ? 0 : (q == 3 ? 2 : 1);
+  const int frow = fwd_blk * B + b;
+  const float mu = ms[(size_t)frow * 2 * L + i];
+  const float s = ms[(size_t)frow * 2 * L + L + i];
+  const float e = eps[((size_t)eps_slot(fwd_blk) * B + b) * L + i];
+  const float sig = sqrtf(expf(s));
+  float dz, dmu_extra = 0.f, ds_extra = 0.f;
+  if (q == 0) {
+    dz = -2.f * w * (zl - zr) * inv_bg;
+  } else if (q == 1) {
+    dz = dzdec[(size_t)b * L + i] + 2.f * w * (zl - zr) * inv_bg;
+    dmu_extra = mu * inv_bg;
+    ds_extra = 0.5f * (expf(s) - 1.f) * inv_bg;
+  } else {
+    const float dr = draw[b];
+    if (metric == 1) {
+      const float d = 2.f * dr * (zl - zk);
+      dz = q == 2 ? d : -d;
+    } else {
+      const float ssl = colsq[i], ssk = colsq[L + i];
+      const float rl = rsqrtf(fmaxf(ssl, L2_EPS)), rk = rsqrtf(fmaxf(ssk, L2_EPS));
+      const float nl = zl * rl, nk = zk * rk, c = coldot[i];
+      if (q == 2) dz = rl * (dr * nk - (ssl >= L2_EPS ? nl * c : 0.f));
+      else        dz = rk * (dr * nl - (ssk >= L2_EPS ? nk * c : 0.f));
+    }
+  }
+  const float dmu = dz + dmu_extra;
+  const float ds = 0.5f * dz * e * sig + ds_extra;
+  dhead[(size_t)r * 2 * L + i] = dmu;
+  dhead[(size_t)r * 2 * L + L + i] = ds;
+  if (dheadh) {
+    dheadh[(size_t)r * 2 * L + i] = __float2bfloat16(dmu);
+    dheadh[(size_t)r * 2 * L + L + i] = __float2bfloat16(ds);
+  }
+}
+
+// ---------------------------------------------------------------- dual TF-Adam
+// opt1 (lr1, g1) over every trained variable, opt2 (lr2, g2) over the encoder slice;
+// both from the pre-step gradients: theta = (theta - d1) - d2.  lr_t precomputed on the
+// host in fp32 exactly as TF ApplyAdam (lr*sqrt(1-b2^t)/(1-b1^t) with fp32 beta powers).
+__global__ void adam_kernel(AdamArgs a) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.n_all) return;
+  float th = a.theta[i];
+  {
+    const float g = a.g1[i];
+    float m = a.m1[i], v = a.v1[i];
+    m += (g - m) * (1.f - a.b1);
+    v += (g * g - v) * (1.f - a.b2);
+    a.m1[i] = m; a.v1[i] = v;
+    th -= (a.lr1 * m) / (sqrtf(v) + a.eps);
+  }
+  if (i < a.n_enc) {
+    const float g = a.g2[i];
+    float m = a.m2[i], v = a.v2[i];
+    m += (g - m) * (1.f - a.b1);
+    v += (g * g - v) * (1.f - a.b2);
+    a.m2[i] = m; a.v2[i] = v;
+    th -= (a.lr2 * m) / (sqrtf(v) + a.eps);
+  }
+  a.theta[i] = th;
+  if (a.theta_h) a.theta_h[i] = __float2bfloat16(th);
+}
+
+__global__ void cast_bf16_kernel(const float* __restrict__ s, __hip_bfloat16* __restrict__ d, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) d[i] = __float2bfloat16(s[i]);
+}
+
+__global__ void copy2d_kernel(const float* __restrict__ s, int lds, float* __restrict__ d, int ldd,
+                              int rows, int cols) {
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)rows * cols) return;
+  const int r = (int)(idx / cols), c = (int)(idx - (size_t)r * cols);
+  d[(size_t)r * ldd + c] = s[(size_t)r * lds + c];
+}
+
+inline unsigned nblocks(size_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
+
+}  // namespace
+
+hipError_t launch_deinterleave(const float* x, float* xs, __hip_bfloat16* xsh, int B, int D,
+                               int ldx, hipStream_t st) {
+  if ((D % 4) == 0 && (reinterpret_cast<uintptr_t>(x) % 16) == 0 && (ldx % 4) == 0) {
+    dim3 g(nblocks(D / 4, 256), B);
+    hipLaunchKernelGGL(deinterleave_vec_kernel, g, dim3(256), 0, st,
+                       reinterpret_cast<const float4*>(x), xs, xsh, B, D, ldx);
+  } else {
+    dim3 g(nblocks(D, 256), B);
+    hipLaunchKernelGGL(deinterleave_scalar_kernel, g, dim3(256), 0, st, x, xs, xsh, B, D, ldx);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_normal(float* out, size_t n, uint64_t seed, uint64_t counter, hipStream_t st) {
+  hipLaunchKernelGGL(normal_kernel, dim3(nblocks((n + 3) / 4, 256)), dim3(256), 0, st, out, n, seed, counter);
+  return hipGetLastError();
+}
+
+hipError_t launch_latent_fwd(const float* ms, const float* eps, float* z, __hip_bfloat16* zh, int B,
+                             int L, int ldz, hipStream_t st) {
+  const size_t n = (size_t)3 * B * L;
+  hipLaunchKernelGGL(latent_fwd_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, ms, eps, z, zh, B, L, ldz);
+  return hipGetLastError();
+}
+
+int colstats_nchunk(int B) { return (B + CS_ROWS - 1) / CS_ROWS; }
+
+hipError_t launch_colstats(int mode, const float* z, int B, int L, int ldz, const float* colsq,
+                           const float* draw, float* part, int nchunk, float* out, hipStream_t st) {
+  const int ncols = mode == 0 ? 2 * L : L;
+  dim3 g(nblocks(ncols, 64), nchunk);
+  hipLaunchKernelGGL(colstats_part_kernel, g, dim3(256), 0, st, mode, z, B, L, ldz, colsq, draw, part);
+  hipLaunchKernelGGL(colstats_final_kernel, dim3(nblocks(ncols, 256)), dim3(256), 0, st, part, nchunk, ncols, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_metric(const float* z, int ldz, const float* ms, const float* rowpart, int nblk,
+                         const float* areas, const float* colsq, int B, int L, int metric, int recip,
+                         float w, float inv_bg, float* rowvals, float* dist, float* draw,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(metric_kernel, dim3(nblocks(B, 4)), dim3(256), 0, st, z, ldz, ms, rowpart, nblk,
+                     areas, colsq, B, L, metric, recip, w, inv_bg, rowvals, dist, draw);
+  return hipGetLastError();
+}
+
+hipError_t launch_loss_reduce(const float* rowvals, int B, float inv_bg, float* losses, hipStream_t st) {
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, st, rowvals, B, inv_bg, losses);
+  return hipGetLastError();
+}
+
+hipError_t launch_latent_bwd(const float* z, int ldz, const float* ms, const float* eps,
+                             const float* dzdec, const float* draw, const float* colsq,
+                             const float* coldot, int B, int L, int metric, float w, float inv_bg,
+                             float* dhead, __hip_bfloat16* dheadh, hipStream_t st) {
+  const size_t n = (size_t)4 * B * L;
+  hipLaunchKernelGGL(latent_bwd_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, z, ldz, ms, eps, dzdec,
+                     draw, colsq, coldot, B, L, metric, w, inv_bg, dhead, dheadh);
+  return hipGetLastError();
+}
+
+hipError_t launch_adam(const AdamArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL(adam_kernel, dim3(nblocks(a.n_all, 256)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_cast_bf16(const float* src, __hip_bfloat16* dst, size_t n, hipStream_t st) {
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, src, dst, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy2d(const float* src, int lds, float* dst, int ldd, int rows, int cols,
+                         hipStream_t st) {
+  const size_t n = (size_t)rows * cols;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(copy2d_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, src, lds, dst, ldd, rows, cols);
+  return hipGetLastError();
+}
+
+}  // namespace mvae

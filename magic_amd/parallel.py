@@ -1,0 +1,63 @@
+"""Data parallelism for the metric-VAE step: one process per GPU, batch rows sharded over
+ranks, full replicas of the parameters and of both Adam states.
+
+The reference has no distributed code; this is the MI355X-native layer.
+Per step and rank (``world`` ranks, local batch B, global batch N*B):
+
+  forward(x_local)                     local encoder/decoder, 1/(N*B) loss scaling
+  all_reduce(colsq)  [cosine only]     2L floats: axis-0 l2_normalize needs sum_b z^2 over
+                                       the GLOBAL batch (``8c/vae.py:449-450``)
+  metric(areas_local)
+  all_reduce(coldot) [cosine only]     L floats: sum_b draw_b n_lock n_key (global)
+  backward()
+  all_reduce(grads)                    ONE bucket [g1 | g2] (RCCL over xGMI on MI355X)
+  adam()                               identical on every rank -> replicas stay bitwise equal
+  all_reduce(losses) (optional)        5 floats, for logging / the NaN guard
+
+The squared-difference metric needs no mid-step collective; the result equals the
+single-process step on the concatenated batch (tests/test_parallel_gloo.py).
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+
+class DataParallelStep:
+    """Drives any engine exposing forward/metric/backward/adam and the tensors
+    ``colsq``, ``coldot``, ``grads``, ``losses`` (the HIP ``Engine``; tests also drive a
+    CPU stand-in built on the oracle)."""
+
+    def __init__(self, engine, group=None, reduce_losses: bool = True):
+        self.e = engine
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.reduce_losses = reduce_losses
+        self.cosine = engine.cfg.metric == "cosine"
+        if engine.cfg.gbatch != engine.cfg.batch * self.world:
+            raise ValueError(f"engine global_batch {engine.cfg.gbatch} != batch {engine.cfg.batch} "
+                             f"x world {self.world}")
+
+    def _ar(self, t):
+        if self.world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+
+    def step(self, x, areas, eps=None):
+        e = self.e
+        e.forward(x, eps)
+        if self.cosine:
+            self._ar(e.colsq)
+        e.metric(areas)
+        if self.cosine:
+            self._ar(e.coldot)
+        e.backward()
+        self._ar(e.grads)
+        e.adam()
+        if self.reduce_losses:
+            self._ar(e.losses)
+        return e.losses
+
+
+def shard_rows(t: torch.Tensor, rank: int, world: int) -> torch.Tensor:
+    n = t.shape[0] // world
+    return t[rank * n:(rank + 1) * n]

@@ -1,0 +1,147 @@
+"""``TangoEncoder`` — drop-in mirror of the reference class (``11a/vae.py:13-441``,
+``8c/vae.py:13-435``) backed by the MI355X HIP step in ``libmvae.so``.
+
+Same constructor entry (``TangoEncoder(sess)``; hyper-parameters via ``config=``), same
+methods and return values:
+
+  partial_fit(X, overlap_areas) -> (cost, training_loss, rec_loss, lat_loss, def_loss, distance)
+                                   (11a, ``:385-411``; 5-tuple without distance when
+                                   ``compat="8c"``, ``8c/vae.py:379-405``)
+  get_predictions(X, overlap_areas) -> distance[B]       (``:413-414``)
+  transform(X, overlap_areas)       -> z_mean[B, L]      (``:416-420``)
+  generate(z_mu=None)               -> x_reconstructed_mean (``:422-434``)
+  reconstruct(X, overlap_areas)     -> x_reconstructed_mean[B, D] (``:436-440``)
+  cosine_distance (module function)  (``:444-458``) — host-side helper for tests/tools
+
+X is ``[B, H*W*3]`` float32, HWC-interleaved (lock, rotated lock, key) exactly as
+``overlap_input.inputs(normalize=True, reshape=True, rotation=True)`` yields it. Inputs may
+be numpy arrays (copied host->device, as ``feed_dict`` did) or float32 device tensors
+(no copy). Outputs are numpy arrays like ``sess.run`` results.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .config import MVAEConfig, preset
+from .constants import FLAGS, metric_name
+from .engine import Engine
+
+
+def _default_config() -> MVAEConfig:
+    # 11a/vae.py:30-65 with the FLAGS of 11a/constants.py
+    return preset("11a", image_size=FLAGS.IMAGE_SIZE, batch=FLAGS.BATCH_SIZE,
+                  metric=metric_name(FLAGS.DISTANCE_METRIC))
+
+
+class TangoEncoder(object):
+    def __init__(self, sess=None, config: Optional[MVAEConfig] = None, device: int = 0,
+                 compat: str = "11a", init_seed: int = 0, data_parallel=None):
+        self.sess = sess  # kept for signature compatibility (11a/vae.py:22)
+        cfg = config or _default_config()
+        self.config = cfg
+        self.encoder_neurons = list(cfg.enc)
+        self.decoder_neurons = list(cfg.dec)
+        assert len(self.encoder_neurons) > 0
+        assert len(self.decoder_neurons) == 2
+        self.num_input_neurons = cfg.D * 3
+        self.latent_dimensions = cfg.latent
+        self.learning_rates = list(cfg.lr)
+        self.batch_size = cfg.batch
+        self.compat = compat
+        self.engine = Engine(cfg, device)
+        self.engine.init_params(init_seed)
+        self._dp = None
+        if data_parallel is not None:
+            from .parallel import DataParallelStep
+            self._dp = DataParallelStep(self.engine, group=None if data_parallel is True else data_parallel)
+        self._losses = torch.empty(5, device=self.engine.dev)
+        self._dist = torch.empty(cfg.batch, device=self.engine.dev)
+
+    # ----------------------------------------------------------------- helpers
+    def _dev(self, a, shape):
+        dev = self.engine.dev
+        if isinstance(a, torch.Tensor):
+            t = a.to(device=dev, dtype=torch.float32)
+        else:
+            t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).to(dev, non_blocking=False)
+        t = t.reshape(shape).contiguous()
+        return t
+
+    def _x(self, X):
+        return self._dev(X, (self.batch_size, self.num_input_neurons))
+
+    # ----------------------------------------------------------------- reference API
+    def partial_fit(self, X, overlap_areas, eps=None):
+        """One training step (both Adam updates). Returns the PRE-update losses."""
+        x = self._x(X)
+        a = self._dev(overlap_areas, (self.batch_size,))
+        e = None if eps is None else self._dev(eps, (3, self.batch_size, self.latent_dimensions))
+        if self._dp is None:
+            self.engine.train_step(x, a, e, losses_out=self._losses, dist_out=self._dist)
+            losses = self._losses
+        else:
+            losses = self._dp.step(x, a, e)
+            self._dist.copy_(self.engine.dist)
+        l = losses.cpu().numpy().astype(np.float64)
+        cost, training_loss, rec_loss, lat_loss, def_loss = (float(v) for v in l[:5])
+        if self.compat == "8c":
+            return cost, training_loss, rec_loss, lat_loss, def_loss
+        return cost, training_loss, rec_loss, lat_loss, def_loss, self._dist.cpu().numpy()
+
+    def get_predictions(self, X, overlap_areas=None, eps=None):
+        e = None if eps is None else self._dev(eps, (3, self.batch_size, self.latent_dimensions))
+        return self.engine.predict(self._x(X), e).cpu().numpy()
+
+    def transform(self, X, overlap_areas=None):
+        return self.engine.transform(self._x(X)).cpu().numpy()
+
+    def generate(self, z_mu=None):
+        if z_mu is None:
+            z_mu = np.random.normal(size=self.latent_dimensions)
+        z = self._dev(z_mu, (-1, self.latent_dimensions))
+        return self.engine.generate(z).cpu().numpy()
+
+    def reconstruct(self, X, overlap_areas=None, eps=None):
+        e = None if eps is None else self._dev(eps, (3, self.batch_size, self.latent_dimensions))
+        return self.engine.reconstruct(self._x(X), e).cpu().numpy()
+
+    # ----------------------------------------------------------------- extras
+    def parameters(self):
+        """Name -> torch view of the device parameters (reference variable meanings)."""
+        return self.engine.params()
+
+    def state_dict(self):
+        out = {f"param/{k}": v.detach().cpu().clone() for k, v in self.engine.params().items()}
+        for kind, tag in ((3, "m1"), (4, "v1"), (5, "m2"), (6, "v2")):
+            for k, v in self.engine.tensors(kind).items():
+                out[f"{tag}/{k}"] = v.detach().cpu().clone()
+        t1, t2 = self.engine.get_step()
+        out["step"] = torch.tensor([t1, t2])
+        return out
+
+    def load_state_dict(self, sd):
+        views = {3: "m1", 4: "v1", 5: "m2", 6: "v2"}
+        for k, v in self.engine.params().items():
+            v.copy_(sd[f"param/{k}"].to(v.device))
+        for kind, tag in views.items():
+            for k, v in self.engine.tensors(kind).items():
+                v.copy_(sd[f"{tag}/{k}"].to(v.device))
+        t1, t2 = (int(x) for x in sd["step"])
+        self.engine.set_step(t1, t2)
+        torch.cuda.synchronize(self.engine.dev)
+
+    def close(self):
+        self.engine.close()
+
+
+def cosine_distance(a, b):
+    """``11a/vae.py:444-458``: l2-normalise along axis 0 (the batch axis), then the row-wise
+    dot product. Host helper (numpy) for tools and tests; the step computes this in HIP."""
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    na = a / np.sqrt(np.maximum((a * a).sum(0, keepdims=True), np.float32(1e-12)))
+    nb = b / np.sqrt(np.maximum((b * b).sum(0, keepdims=True), np.float32(1e-12)))
+    return (na * nb).sum(1)

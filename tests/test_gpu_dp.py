@@ -1,0 +1,74 @@
+"""Data-parallel step on the real HIP kernels: 2 ranks sharing the box's one GPU (gloo
+all-reduce of device tensors), each with half the batch, vs one process on the full
+batch. The all-reduced gradient bucket and the global losses must match the single-
+process step within the fp32 parity tolerance (1e-4 relative)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from magic_amd.config import preset
+from tests.gpu_helpers import make_inputs, make_params, max_rel
+
+pytestmark = pytest.mark.gpu
+
+
+def _worker(rank, world, port, metric, q):
+    import torch.distributed as dist
+    from magic_amd.engine import Engine
+    from magic_amd.parallel import DataParallelStep
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = preset("8c", image_size=24, batch=32, metric=metric)
+    B = cfg.batch
+    half = B // world
+    eng = Engine(cfg.replace(batch=half, global_batch=B), 0)
+    eng.load_params(make_params(cfg))
+    X, areas, eps = make_inputs(cfg, B)
+    sl = slice(rank * half, (rank + 1) * half)
+    st = DataParallelStep(eng)
+    st.step(torch.from_numpy(X[sl]).cuda(), torch.from_numpy(areas[sl]).cuda(),
+            torch.from_numpy(np.ascontiguousarray(eps[:, sl])).cuda())
+    torch.cuda.synchronize()
+    q.put((rank, eng.grads.cpu().numpy(), eng.losses.cpu().numpy()))
+    eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("metric", ["cosine", "sqdiff"])
+def test_dp2_on_gpu_matches_full_batch(metric):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from magic_amd.engine import Engine
+    cfg = preset("8c", image_size=24, batch=32, metric=metric)
+    eng = Engine(cfg, 0)
+    eng.load_params(make_params(cfg))
+    X, areas, eps = make_inputs(cfg, cfg.batch)
+    eng.forward(torch.from_numpy(X).cuda(), torch.from_numpy(eps).cuda())
+    eng.metric(torch.from_numpy(areas).cuda())
+    eng.backward()
+    torch.cuda.synchronize()
+    g_ref, l_ref = eng.grads.cpu().numpy(), eng.losses.cpu().numpy()
+    eng.close()
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, metric, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (g, l)) for r, g, l in (q.get(timeout=300) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r in range(2):
+        g, l = res[r]
+        np.testing.assert_allclose(l, l_ref, rtol=1e-4)
+        assert max_rel(g, g_ref) <= 1e-4
+    np.testing.assert_array_equal(res[0][0], res[1][0])

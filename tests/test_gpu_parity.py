@@ -1,0 +1,271 @@
+"""HIP path vs the oracle on the same seeded inputs (fp32 GPU vs float64 CPU restatement).
+
+Tolerance (BASELINE.json north_star): 1e-4 relative, fp32. Written per tensor as
+max|gpu - oracle| <= 1e-4 * max|oracle| (max-norm relative), for the five losses, the
+distance vector, every gradient of both optimizers and the Adam-updated parameters.
+"""
+import numpy as np
+import pytest
+import torch
+
+from magic_amd import _lib
+from magic_amd.config import MVAEConfig, preset
+from oracle import mvae_oracle as O
+from tests.gpu_helpers import (gpu_phases, make_inputs, make_params, max_rel, oracle_cfg,
+                               oracle_phases, to_dev)
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-4
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def _engine(cfg):
+    from magic_amd.engine import Engine
+    return Engine(cfg, 0)
+
+
+# ------------------------------------------------------------------ GEMM family
+@pytest.mark.parametrize("at,bt", [(0, 0), (1, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (37, 53, 29), (128, 128, 32), (300, 517, 1001),
+                                   (129, 40, 8193), (501, 20, 64)])
+def test_gemm_layouts(at, bt, M, N, K):
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(M * 7 + N * 3 + K)
+    A = torch.randn((K, M) if at else (M, K), device="cuda", generator=g)
+    Bm = torch.randn((N, K) if bt else (K, N), device="cuda", generator=g)
+    C = torch.full((M, N), float("nan"), device="cuda")
+    rc = lib.mvae_debug_gemm(M, N, K, A.data_ptr(), A.shape[1], at, Bm.data_ptr(), Bm.shape[1], bt,
+                             C.data_ptr(), N, 0, 0, None, 0, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, lib.mvae_last_error(None)
+    ref = (A.double().T if at else A.double()) @ (Bm.double().T if bt else Bm.double())
+    err = (C.double() - ref).abs().max().item()
+    # exact-fp32 MFMA (k-ordered fma chain): error ~ 1e-7 * sum|a*b|
+    bound = 2e-6 * ((A.double().abs().T if at else A.double().abs()) @
+                    (Bm.double().abs().T if bt else Bm.double().abs())).max().item() + 1e-6
+    assert err <= bound, (err, bound)
+
+
+@pytest.mark.parametrize("epi,act", [(1, 0), (1, 1), (2, 0), (2, 1), (4, 0)])
+def test_gemm_epilogues(epi, act):
+    lib = _lib.load()
+    M, N, K = 200, 130, 77
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.randn(M, K, device="cuda", generator=g) * 0.3
+    Bm = torch.randn(K, N, device="cuda", generator=g) * 0.3
+    aux = torch.tanh(torch.randn(M, N, device="cuda", generator=g)) if act == 0 else \
+        torch.nn.functional.elu(torch.randn(M, N, device="cuda", generator=g))
+    C = torch.empty(M, N, device="cuda")
+    rc = lib.mvae_debug_gemm(M, N, K, A.data_ptr(), K, 0, Bm.data_ptr(), N, 0, C.data_ptr(), N, epi,
+                             act, aux.data_ptr(), N, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    acc = A.double() @ Bm.double()
+    if epi == 1:
+        ref = torch.tanh(acc) if act == 0 else torch.where(acc < 0, torch.exp(acc) - 1, acc)
+    elif epi == 2:
+        a = aux.double()
+        ref = acc * (1 - a * a) if act == 0 else torch.where(a < 0, acc * (a + 1), acc)
+    else:
+        ref = torch.sigmoid(acc)
+    assert (C.double() - ref).abs().max().item() < 1e-5
+
+
+# ------------------------------------------------------------------ full step
+def tiny(act, metric, recip, w, **kw):
+    base = dict(image_size=12, batch=24, enc=(40, 36, 24), dec=(28, 20), latent=6, act=act,
+                metric=metric, reciprocal=recip, deform_weight=w, lr=(1e-3, 1e-4))
+    base.update(kw)
+    return MVAEConfig(**base)
+
+
+FLAVOURS = [
+    ("tanh", "cosine", False, 10.0),   # 8c / 8d / 8e
+    ("tanh", "cosine", True, 10.0),    # 9a / 10a
+    ("elu", "sqdiff", True, 100.0),    # 10b / 11a
+    ("tanh", "sqdiff", False, 10.0),
+    ("elu", "cosine", False, 100.0),
+]
+
+
+def check_step(cfg, seed=1, density=0.1, tol=TOL, adam=True):
+    eng = _engine(cfg)
+    try:
+        P = make_params(cfg)
+        eng.load_params(P)
+        X, areas, eps = make_inputs(cfg, cfg.batch, seed=seed, density=density)
+        lg, dg, g1g, g2g = gpu_phases(eng, X, areas, eps)
+        lo, do, g1o, g2o, oc_cache = oracle_phases(cfg, P, X, areas, eps)
+        m1, m2 = oc_cache["mag"]
+        for i, nm in enumerate(("cost", "training_loss", "r_l", "l_l", "d_l")):
+            assert abs(lg[i] - lo[i]) <= tol * max(abs(lo[i]), 1e-3), (nm, lg[i], lo[i])
+        assert max_rel(dg, do) <= tol, ("distance", max_rel(dg, do))
+        for k in O.trained_names(oracle_cfg(cfg)):
+            e = max_rel(g1g[k], g1o[k], m1[k])
+            assert e <= tol, ("g1", k, e)
+        for k in O.encoder_names(oracle_cfg(cfg)):
+            e = max_rel(g2g[k], g2o[k], m2[k])
+            assert e <= tol, ("g2", k, e)
+        assert set(g2g) == set(O.encoder_names(oracle_cfg(cfg)))
+        if adam:
+            # Adam kernel vs TF ApplyAdam restated, both fed the GPU's own gradients (the
+            # gradients themselves were checked above; the first step ~ lr*sign(g) would
+            # otherwise amplify fp32 noise on near-zero gradients).
+            oc = oracle_cfg(cfg)
+            st = O.adam_init(oc, P)
+            Pn, _ = O.adam({k: P[k].astype(np.float64) for k in P}, g1g, g2g, st, oc)
+            eng.adam()
+            torch.cuda.synchronize()
+            Pg = {k: v.cpu().numpy().astype(np.float64) for k, v in eng.params().items()}
+            scale = sum(cfg.lr)
+            for k in O.trained_names(oc):
+                err = np.abs(Pg[k] - Pn[k])
+                assert np.all(err <= 1e-4 * scale + 2e-7 * np.abs(P[k])), (k, err.max())
+                assert np.all(np.abs(Pg[k] - P[k]) <= 1.01 * scale + 1e-6), k
+            for k in O.DEAD:
+                np.testing.assert_array_equal(Pg[k], P[k])  # dead variables: never trained
+        return eng
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("flav", FLAVOURS)
+def test_step_tiny(flav):
+    check_step(tiny(*flav))
+
+
+def test_step_latent2_odd_image():
+    """9a-style L=2 (2L=4, ld padding) and an odd image (D=49: scalar de-interleave)."""
+    check_step(tiny("tanh", "cosine", True, 10.0, image_size=7, latent=2, batch=9))
+
+
+def test_step_batch_of_one_cosine():
+    """B=1 cosine: columns normalise to +-1 (KAT (v)); exercises single-row reductions."""
+    check_step(tiny("tanh", "cosine", False, 10.0, batch=1), adam=False)
+
+
+def test_step_c1_full_width():
+    """BASELINE C1: 8c preset at 100x100 (D=1e4), enc [500]*4, L=20, B=64."""
+    check_step(preset("8c", image_size=100, batch=64))
+
+
+def test_step_11a_full_width():
+    check_step(preset("11a", image_size=100, batch=48))
+
+
+def test_step_c2_batch4096():
+    """BASELINE C2 (fp32, B=4096): the benched configuration, full size, against float64."""
+    check_step(preset("8c", image_size=100, batch=4096), adam=False)
+
+
+def test_multi_step_losses_track_oracle():
+    cfg = preset("8c", image_size=40, batch=32)
+    eng = _engine(cfg)
+    try:
+        P = make_params(cfg)
+        eng.load_params(P)
+        oc = oracle_cfg(cfg)
+        Po = {k: v.astype(np.float64) for k, v in P.items()}
+        st = O.adam_init(oc, Po)
+        out = torch.empty(5, device="cuda")
+        for s in range(4):
+            X, areas, eps = make_inputs(cfg, cfg.batch, seed=10 + s)
+            eng.train_step(to_dev(X), to_dev(areas), to_dev(eps), losses_out=out)
+            lo, dist, Po, st, _ = O.train_step(Po, st, X, areas, eps, oc)
+            lg = out.cpu().numpy()
+            np.testing.assert_allclose(lg, lo, rtol=1e-3)
+        assert eng.get_step() == (4, 4)
+    finally:
+        eng.close()
+
+
+def test_determinism_bitwise():
+    """Same inputs twice -> bitwise identical gradients and losses (no float atomics)."""
+    cfg = preset("8c", image_size=30, batch=200)
+    eng = _engine(cfg)
+    try:
+        P = make_params(cfg)
+        X, areas, eps = make_inputs(cfg, cfg.batch)
+        outs = []
+        for _ in range(2):
+            eng.load_params(P)
+            outs.append(gpu_phases(eng, X, areas, eps))
+        for a, b in zip(outs[0][:2], outs[1][:2]):
+            np.testing.assert_array_equal(a, b)
+        for k in outs[0][2]:
+            np.testing.assert_array_equal(outs[0][2][k], outs[1][2][k])
+    finally:
+        eng.close()
+
+
+def test_internal_eps_is_standard_normal():
+    cfg = tiny("tanh", "sqdiff", False, 10.0, batch=512, latent=64)
+    eng = _engine(cfg)
+    try:
+        X, _, _ = make_inputs(cfg, cfg.batch)
+        eng.forward(to_dev(X), None)
+        e1 = eng.buffer(_lib.BUF_EPS).clone()
+        eng.forward(to_dev(X), None)
+        e2 = eng.buffer(_lib.BUF_EPS).clone()
+        torch.cuda.synchronize()
+        assert not torch.equal(e1, e2)
+        v = e1.double()
+        assert abs(v.mean().item()) < 0.02 and abs(v.std().item() - 1) < 0.02
+        assert abs(((v ** 4).mean() - 3).item()) < 0.15
+    finally:
+        eng.close()
+
+
+def test_inference_surface_matches_oracle():
+    cfg = preset("11a", image_size=20, batch=16)
+    eng = _engine(cfg)
+    try:
+        P = make_params(cfg)
+        eng.load_params(P)
+        oc = oracle_cfg(cfg)
+        X, areas, eps = make_inputs(cfg, cfg.batch)
+        x = to_dev(X)
+        dist = eng.predict(x, to_dev(eps)).cpu().numpy()
+        assert max_rel(dist, O.predictions(P, X, eps, oc)) <= TOL
+        zm = eng.transform(x).cpu().numpy()
+        _, mu, _ = O.encode({k: v.astype(np.float64) for k, v in P.items()}, X[:, 0::3].astype(np.float64), oc)
+        assert max_rel(zm, mu) <= TOL
+        y = eng.reconstruct(x, to_dev(eps)).cpu().numpy()
+        c = O.forward(P, X, eps, oc)
+        assert max_rel(y, c["y"]) <= TOL
+        z = np.random.default_rng(3).standard_normal((5, cfg.latent)).astype(np.float32)
+        yg = eng.generate(to_dev(z)).cpu().numpy()
+        _, _, _, yo = O.decode({k: v.astype(np.float64) for k, v in P.items()}, z.astype(np.float64), oc)
+        assert max_rel(yg, yo) <= TOL
+    finally:
+        eng.close()
+
+
+def test_tango_encoder_api():
+    from magic_amd.vae import TangoEncoder
+    cfg = preset("11a", image_size=20, batch=8)
+    vae = TangoEncoder(None, config=cfg)
+    X, areas, _ = make_inputs(cfg, cfg.batch)
+    out = vae.partial_fit(X, areas)
+    assert len(out) == 6 and out[5].shape == (8,)
+    assert all(np.isfinite(v) for v in out[:5])
+    assert vae.get_predictions(X, areas).shape == (8,)
+    assert vae.transform(X, areas).shape == (8, cfg.latent)
+    assert vae.reconstruct(X, areas).shape == (8, cfg.D)
+    assert vae.generate().shape == (1, cfg.D)
+    sd = vae.state_dict()
+    vae2 = TangoEncoder(None, config=cfg, init_seed=5)
+    vae2.load_state_dict(sd)
+    e = np.random.default_rng(0).standard_normal((3, 8, cfg.latent)).astype(np.float32)
+    a = vae.partial_fit(X, areas, eps=e)
+    b = vae2.partial_fit(X, areas, eps=e)
+    np.testing.assert_array_equal(np.array(a[:5]), np.array(b[:5]))
+    vae.close()
+    vae2.close()
+    v8 = TangoEncoder(None, config=preset("8c", image_size=20, batch=8), compat="8c")
+    assert len(v8.partial_fit(X, areas)) == 5
+    v8.close()
