@@ -42,7 +42,10 @@ extern "C" {
 enum { MVAE_OK = 0, MVAE_EINVAL = -1, MVAE_ECONFIG = -2, MVAE_ESTATE = -3 };
 enum { MVAE_ACT_TANH = 0, MVAE_ACT_ELU = 1 };                    /* 8c family : 11a */
 enum { MVAE_METRIC_COSINE = 0, MVAE_METRIC_SQDIFF = 1 };        /* 11a/constants.py:5-7 */
-enum { MVAE_PREC_F32 = 0, MVAE_PREC_BF16 = 1 };                 /* GEMM operand precision */
+/* GEMM arithmetic: F32 = native fp32 MFMA; BF16 = bf16 operands, fp32 accumulate;
+ * F32X = fp32-accurate: every fp32 operand split exactly into 3 bf16 terms, products
+ * a_i*b_j with i+j<3 on bf16 MFMA, fp32 accumulate (exact-bf16 tiles take 1 term). */
+enum { MVAE_PREC_F32 = 0, MVAE_PREC_BF16 = 1, MVAE_PREC_F32X = 2 };
 
 /* Hyper-parameters the reference hard-codes in TangoEncoder.__init__ (11a/vae.py:30-65)
  * and FLAGS (11a/constants.py:32,49,52,60). */
@@ -141,8 +144,11 @@ int mvae_timing_read(mvae_ctx* ctx, int region, double* total_ms, int64_t* count
 int mvae_timing_reset(mvae_ctx* ctx);
 /* One GEMM of the step's kernel family: C[M,N] = epi(A[M,K] B[K,N]); A stored [M][K]
  * (at=0) or [K][M] (at=1), B stored [K][N] (bt=0) or [N][K] (bt=1). epi: 0 store,
- * 1 act (act: 0 tanh, 1 elu), 2 C = acc * act'(aux), 4 sigmoid. split_k: 0 = planner's
- * choice. Workspace is allocated and freed inside (synchronous; tests only).           */
+ * 1 act (act: 0 tanh, 1 elu), 2 C = acc * act'(aux), 4 sigmoid; epi | (prec << 4)
+ * selects the arithmetic (MVAE_PREC_*). Workspace is allocated and freed inside
+ * (synchronous; tests only). mvae_bench_gemm: variant | (prec << 4).                 */
+int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, int variant, int iters,
+                    void* stream, float* avg_ms);
 int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int at, const float* B, int ldb,
                     int bt, float* C, int ldc, int epi, int act, const float* aux, int ld_aux,
                     void* stream);

@@ -17,7 +17,7 @@ ABI_VERSION = 1
 
 ACT = {"tanh": 0, "elu": 1}
 METRIC = {"cosine": 0, "sqdiff": 1}
-PREC = {"f32": 0, "bf16": 1}
+PREC = {"f32": 0, "bf16": 1, "f32x": 2}
 
 KIND_PARAM, KIND_GRAD1, KIND_GRAD2, KIND_M1, KIND_V1, KIND_M2, KIND_V2 = range(7)
 (BUF_PARAMS, BUF_GRADS, BUF_ADAM, BUF_LOSSES, BUF_COLSQ, BUF_COLDOT, BUF_DIST, BUF_GRADS_DEC,
@@ -76,6 +76,8 @@ _SIGS = {
     "mvae_timing_name": ([C.c_void_p, C.c_int], C.c_char_p),
     "mvae_timing_read": ([C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)], C.c_int),
     "mvae_timing_reset": ([C.c_void_p], C.c_int),
+    "mvae_bench_gemm": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                         C.c_void_p, C.POINTER(C.c_float)], C.c_int),
     "mvae_debug_gemm": ([C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
                          C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                          C.c_int, C.c_void_p], C.c_int),

@@ -94,7 +94,7 @@ def baseline_config(cid: str) -> MVAEConfig:
     if cid == "C2":
         return preset("8c", batch=4096)
     if cid in ("C3", "C4"):
-        return preset("8d", batch=8192)
+        return preset("8d", batch=8192, precision="bf16")
     if cid == "C5":
-        return preset("8e", batch=8192, metric="sqdiff", reciprocal=True)
+        return preset("8e", batch=8192, metric="sqdiff", reciprocal=True, precision="bf16")
     raise KeyError(cid)

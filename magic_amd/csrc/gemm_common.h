@@ -1,0 +1,135 @@
+// Shared pieces of the GEMM kernel families (fp32 MFMA and bf16 MFMA): launch parameters,
+// activation math with TF semantics, the XCD-grouped tile order and the fused epilogues.
+// Both families use 128x128 workgroup tiles, 4 waves in 2x2, each wave 2x2 MFMA 32x32
+// accumulators, so the accumulator -> (row, col) map and the epilogue are identical.
+#pragma once
+#include "mvae_internal.h"
+
+namespace mvae {
+namespace gemm {
+
+constexpr int BM = 128, BN = 128, NT = 256;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+struct Params {
+  int M, N, K;
+  const float* A; int lda;
+  const float* B; int ldb;
+  float* C; int ldc;
+  long long sA, sB, sC;     // batch strides
+  int batch, split, kchunk;
+  int ntm, ntn;
+  GemmEpi epi;
+};
+
+__device__ __forceinline__ float act_f(float v, int act) {
+  if (act == ACT_TANH) return tanhf(v);
+  return v < 0.f ? expf(v) - 1.f : v;  // TF elu: exp(x) - 1 for x < 0
+}
+__device__ __forceinline__ float dact_f(float g, float y, int act) {
+  if (act == ACT_TANH) return g * (1.f - y * y);  // TF TanhGrad
+  return y < 0.f ? g * (y + 1.f) : g;              // TF EluGrad (on the output)
+}
+__device__ __forceinline__ float sigmoid_f(float v) { return 1.f / (1.f + expf(-v)); }
+
+// bijective XCD remap: consecutive logical tiles land on the same XCD (blockIdx % 8 group)
+__device__ __forceinline__ int xcd_remap(int b, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = b & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+// logical tile of this workgroup
+struct Tile {
+  int z, bi, si, m0, n0, nt, ks, ke;
+};
+__device__ __forceinline__ Tile tile_of(const Params& p, bool remap) {
+  Tile t;
+  const int tiles = p.ntm * p.ntn;
+  const int nwg = tiles * p.batch * p.split;
+  const int b = remap ? xcd_remap(blockIdx.x, nwg) : (int)blockIdx.x;
+  t.z = b / tiles;
+  const int rem = b - t.z * tiles;
+  const int mt = rem / p.ntn;
+  t.nt = rem - mt * p.ntn;
+  t.bi = t.z / p.split;
+  t.si = t.z - t.bi * p.split;
+  t.m0 = mt * BM;
+  t.n0 = t.nt * BN;
+  t.ks = t.si * p.kchunk;
+  t.ke = min(p.K, t.ks + p.kchunk);
+  return t;
+}
+
+// Epilogue over the 2x2 32x32 accumulators of this wave.
+// C/D layout of a 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+// `red` must be >= 2*BM floats of LDS no longer used by the main loop (BCE only).
+template <int EPI>
+__device__ __forceinline__ void epilogue(const Params& p, const Tile& t, f32x16 (&acc)[2][2],
+                                         float* red) {
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int fr = lane & 31, fk = lane >> 5;
+  float* __restrict__ C = p.C + (size_t)t.z * p.sC;  // z = bi*split + si (slab) or bi (split==1)
+  const int rbase = t.m0 + wm * 64 + 4 * fk;
+  const int cbase = t.n0 + wn * 64 + fr;
+  if constexpr (EPI == EPI_BCE) {
+    const GemmEpi& e = p.epi;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + mi * 32 + (r & 3) + 8 * (r >> 2);
+        float rs = 0.f;
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          const int col = cbase + ni * 32;
+          if (row < p.M && col < p.N) {
+            const float yv = sigmoid_f(acc[mi][ni][r]);
+            const float xv = e.x[(size_t)row * e.ldx + col];
+            // -log(y^x (1-y)^(1-x)) with TF pow(0,0) = 1 (no epsilon), 11a/vae.py:266-269
+            float term = 0.f;
+            if (xv != 0.f) term += xv * logf(yv);
+            if (xv != 1.f) term += (1.f - xv) * logf(1.f - yv);
+            rs += term;
+            C[(size_t)row * p.ldc + col] = (yv - xv) * e.scale;
+            if (e.y) e.y[(size_t)row * e.ldy + col] = yv;
+          }
+        }
+#pragma unroll
+        for (int off = 16; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
+        if (fr == 0) red[wn * BM + (row - t.m0)] = rs;  // lanes 0 and 32
+      }
+    }
+    __syncthreads();
+    if (tid < BM && t.m0 + tid < p.M) {
+      e.rowpart[(size_t)(t.m0 + tid) * p.ntn + t.nt] = -(red[tid] + red[BM + tid]);
+    }
+  } else {
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rbase + mi * 32 + (r & 3) + 8 * (r >> 2);
+        if (row >= p.M) continue;
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          const int col = cbase + ni * 32;
+          if (col >= p.N) continue;
+          float v = acc[mi][ni][r];
+          if constexpr (EPI == EPI_ACT) v = act_f(v, p.epi.act);
+          if constexpr (EPI == EPI_SIGMOID) v = sigmoid_f(v);
+          if constexpr (EPI == EPI_DACT) {
+            const int ar = row >= p.epi.remap_split ? row - p.epi.remap_shift : row;
+            v = dact_f(v, p.epi.aux[(size_t)ar * p.epi.ld_aux + col], p.epi.act);
+          }
+          C[(size_t)row * p.ldc + col] = v;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace gemm
+}  // namespace mvae

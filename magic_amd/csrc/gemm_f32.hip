@@ -16,7 +16,7 @@
 // Blocks are remapped so that the column tiles of one row panel share an XCD (L2 reuse of A).
 // Split-K (for small grids) writes fp32 partial slabs that a second kernel sums in a fixed
 // order and passes through the epilogue: results are deterministic run to run.
-#include "mvae_internal.h"
+#include "gemm_common.h"
 
 #include <algorithm>
 #include <cmath>
@@ -24,36 +24,8 @@
 namespace mvae {
 namespace {
 
-constexpr int BM = 128, BN = 128, BK = 32, NT = 256;
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-
-struct Params {
-  int M, N, K;
-  const float* A; int lda;
-  const float* B; int ldb;
-  float* C; int ldc;
-  long long sA, sB, sC;     // batch strides
-  int batch, split, kchunk;
-  int ntm, ntn;
-  GemmEpi epi;
-};
-
-__device__ __forceinline__ float act_f(float v, int act) {
-  if (act == ACT_TANH) return tanhf(v);
-  return v < 0.f ? expf(v) - 1.f : v;  // TF elu: exp(x) - 1 for x < 0
-}
-__device__ __forceinline__ float dact_f(float g, float y, int act) {
-  if (act == ACT_TANH) return g * (1.f - y * y);  // TF TanhGrad
-  return y < 0.f ? g * (y + 1.f) : g;              // TF EluGrad (on the output)
-}
-__device__ __forceinline__ float sigmoid_f(float v) { return 1.f / (1.f + expf(-v)); }
-
-// bijective XCD remap: consecutive logical tiles land on the same XCD (blockIdx % 8 group)
-__device__ __forceinline__ int xcd_remap(int b, int nwg) {
-  const int q = nwg >> 3, r = nwg & 7, xcd = b & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-}
+using namespace gemm;
+constexpr int BK = 32;
 
 template <bool KCONTIG, int SLD, int ROWS>
 struct TileLoader;
@@ -131,7 +103,9 @@ struct TileLoader<false, SLD, ROWS> {
   }
 };
 
-template <bool AT, bool BT, int EPI>
+// VAR (diagnostic A/B variants, EPI_STORE only): 0 default; 1 fragments read per k-step
+// (no read-ahead); 2 no XCD remap.
+template <bool AT, bool BT, int EPI, int VAR = 0>
 __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(Params p) {
   constexpr bool A_KC = !AT;  // A stored [M][K] -> k-contiguous
   constexpr bool B_KC = BT;   // B stored [N][K] -> k-contiguous
@@ -146,16 +120,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(Params p) {
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
 
-  const int tiles = p.ntm * p.ntn;
-  const int nwg = tiles * p.batch * p.split;
-  const int t = xcd_remap(blockIdx.x, nwg);
-  const int z = t / tiles;
-  const int rem = t - z * tiles;
-  const int mt = rem / p.ntn, nt = rem - mt * p.ntn;
-  const int bi = z / p.split, si = z - bi * p.split;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int ks = si * p.kchunk;
-  const int ke = min(p.K, ks + p.kchunk);
+  const Tile t = tile_of(p, VAR != 2);
+  const int bi = t.bi, m0 = t.m0, n0 = t.n0, ks = t.ks, ke = t.ke;
 
   const float* __restrict__ A = p.A + bi * p.sA;
   const float* __restrict__ Bm = p.B + bi * p.sB;
@@ -188,17 +154,37 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(Params p) {
       la.load(A, p.lda, m0, p.M, ks + (kt + 1) * BK, ke, tid);
       lb.load(Bm, p.ldb, n0, p.N, ks + (kt + 1) * BK, ke, tid);
     }
-    const float* as = As + cur * A_TILE + wm * 64 + fr;
-    const float* bs = Bs + cur * B_TILE + wn * 64 + fr;
+    const float* as = As + cur * A_TILE + wm * 64 + fr + fk * SA;
+    const float* bs = Bs + cur * B_TILE + wn * 64 + fr + fk * SB;
+    if constexpr (VAR == 1) {
 #pragma unroll
-    for (int kk = 0; kk < BK / 2; ++kk) {
-      const int k = 2 * kk + fk;
-      const float a0 = as[k * SA], a1 = as[k * SA + 32];
-      const float b0 = bs[k * SB], b1 = bs[k * SB + 32];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      for (int kk = 0; kk < BK / 2; ++kk) {
+        const float a0 = as[2 * kk * SA], a1 = as[2 * kk * SA + 32];
+        const float b0 = bs[2 * kk * SB], b1 = bs[2 * kk * SB + 32];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+    } else {
+      // read the whole k-tile's fragments first (distinct registers), then the MFMA chain:
+      // the LDS latency overlaps the MFMAs instead of serialising every group of four
+      float fa[BK / 2][2], fb[BK / 2][2];
+#pragma unroll
+      for (int kk = 0; kk < BK / 2; ++kk) {
+        fa[kk][0] = as[2 * kk * SA];
+        fa[kk][1] = as[2 * kk * SA + 32];
+        fb[kk][0] = bs[2 * kk * SB];
+        fb[kk][1] = bs[2 * kk * SB + 32];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kk = 0; kk < BK / 2; ++kk) {
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk][0], fb[kk][0], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk][0], fb[kk][1], acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk][1], fb[kk][0], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk][1], fb[kk][1], acc[1][1], 0, 0, 0);
+      }
     }
     if (more) {
       la.store(As + (cur ^ 1) * A_TILE, tid);
@@ -207,68 +193,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(Params p) {
     __syncthreads();
   }
 
-  // ---------------------------------------------------------------- epilogue
-  // C/D layout of 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
-  float* __restrict__ C = p.C + (size_t)z * p.sC;  // z = bi*split + si (slab) or bi (split==1)
-  const int rbase = m0 + wm * 64 + 4 * fk;
-  const int cbase = n0 + wn * 64 + fr;
-  if constexpr (EPI == EPI_BCE) {
-    const GemmEpi& e = p.epi;
-    float* red = smem;  // reuse LDS: [2][BM] row sums of the two column waves
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rbase + mi * 32 + (r & 3) + 8 * (r >> 2);
-        float rs = 0.f;
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          const int col = cbase + ni * 32;
-          if (row < p.M && col < p.N) {
-            const float yv = sigmoid_f(acc[mi][ni][r]);
-            const float xv = e.x[(size_t)row * e.ldx + col];
-            // -log(y^x (1-y)^(1-x)) with TF pow(0,0) = 1 (no epsilon), 11a/vae.py:266-269
-            float term = 0.f;
-            if (xv != 0.f) term += xv * logf(yv);
-            if (xv != 1.f) term += (1.f - xv) * logf(1.f - yv);
-            rs += term;
-            C[(size_t)row * p.ldc + col] = (yv - xv) * e.scale;
-            if (e.y) e.y[(size_t)row * e.ldy + col] = yv;
-          }
-        }
-#pragma unroll
-        for (int off = 16; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
-        if (fr == 0) red[wn * BM + (row - m0)] = rs;  // lanes 0 and 32
-      }
-    }
-    __syncthreads();
-    if (tid < BM && m0 + tid < p.M) {
-      e.rowpart[(size_t)(m0 + tid) * p.ntn + nt] = -(red[tid] + red[BM + tid]);
-    }
-    return;
-  } else {
-#pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rbase + mi * 32 + (r & 3) + 8 * (r >> 2);
-        if (row >= p.M) continue;
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          const int col = cbase + ni * 32;
-          if (col >= p.N) continue;
-          float v = acc[mi][ni][r];
-          if constexpr (EPI == EPI_ACT) v = act_f(v, p.epi.act);
-          if constexpr (EPI == EPI_SIGMOID) v = sigmoid_f(v);
-          if constexpr (EPI == EPI_DACT) {
-            const int ar = row >= p.epi.remap_split ? row - p.epi.remap_shift : row;
-            v = dact_f(v, p.epi.aux[(size_t)ar * p.epi.ld_aux + col], p.epi.act);
-          }
-          C[(size_t)row * p.ldc + col] = v;
-        }
-      }
-    }
-  }
+  epilogue<EPI>(p, t, acc, smem);
 }
 
 // sum split-K slabs in fixed order and apply the epilogue
@@ -295,19 +220,27 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, in
   }
 }
 
-template <bool AT, bool BT, int EPI>
+template <bool AT, bool BT, int EPI, int VAR>
 hipError_t launch_t(const Params& p, hipStream_t st) {
   const int nwg = p.ntm * p.ntn * p.batch * p.split;
-  hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, EPI>), dim3(nwg), dim3(NT), 0, st, p);
+  hipLaunchKernelGGL((gemm_f32_kernel<AT, BT, EPI, VAR>), dim3(nwg), dim3(NT), 0, st, p);
   return hipGetLastError();
 }
 
-template <int EPI>
+template <int EPI, int VAR = 0>
 hipError_t launch_layout(const Params& p, bool at, bool bt, hipStream_t st) {
-  if (!at && !bt) return launch_t<false, false, EPI>(p, st);
-  if (at && !bt) return launch_t<true, false, EPI>(p, st);
-  if (!at && bt) return launch_t<false, true, EPI>(p, st);
-  return launch_t<true, true, EPI>(p, st);
+  if (!at && !bt) return launch_t<false, false, EPI, VAR>(p, st);
+  if (at && !bt) return launch_t<true, false, EPI, VAR>(p, st);
+  if (!at && bt) return launch_t<false, true, EPI, VAR>(p, st);
+  return launch_t<true, true, EPI, VAR>(p, st);
+}
+
+hipError_t launch_store(const Params& p, bool at, bool bt, int variant, hipStream_t st) {
+  switch (variant) {
+    case 1: return launch_layout<EPI_STORE, 1>(p, at, bt, st);
+    case 2: return launch_layout<EPI_STORE, 2>(p, at, bt, st);
+    default: return launch_layout<EPI_STORE, 0>(p, at, bt, st);
+  }
 }
 
 }  // namespace
@@ -323,7 +256,8 @@ int gemm_plan_split(const GemmDesc& d, size_t max_ws) {
   // overlap each other's stalls but share the MFMA pipes), each WG costs its k-tiles plus a
   // fixed prologue/epilogue; split-K adds the slab round trip and one reduction launch.
   const double cus = 256.0;
-  const double t_ktile = 1.75e-6;  // one 128x128x32 fp32 k-tile at the CU's MFMA rate
+  // one 128x128x32 k-tile per CU: fp32 MFMA rate; bf16 / 3-term split are load-bound
+  const double t_ktile = d.prec == GEMM_F32 ? 1.75e-6 : (d.prec == GEMM_BF16 ? 0.3e-6 : 0.5e-6);
   double best = 1e30;
   int best_s = 1;
   for (int s = 1; s <= 32; ++s) {
@@ -351,14 +285,15 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   p.batch = d.batch;
   p.ntm = (d.M + BM - 1) / BM; p.ntn = (d.N + BN - 1) / BN;
   p.epi = d.epi;
-  const int split = gemm_plan_split(d, ws ? ws_elems : 0);
+  const int split = d.split > 0 ? d.split : gemm_plan_split(d, ws ? ws_elems : 0);
   p.split = split;
   const int ktiles = (d.K + BK - 1) / BK;
   p.kchunk = ((ktiles + split - 1) / split) * BK;
   if (split == 1) {
     p.C = d.C; p.ldc = d.ldc; p.sC = d.sC;
+    if (d.prec != GEMM_F32) return gemm_bf16_launch(p, d.at, d.bt, d.prec, d.epi.mode, st);
     switch (d.epi.mode) {
-      case EPI_STORE: return launch_layout<EPI_STORE>(p, d.at, d.bt, st);
+      case EPI_STORE: return launch_store(p, d.at, d.bt, d.variant, st);
       case EPI_ACT: return launch_layout<EPI_ACT>(p, d.at, d.bt, st);
       case EPI_DACT: return launch_layout<EPI_DACT>(p, d.at, d.bt, st);
       case EPI_BCE: return launch_layout<EPI_BCE>(p, d.at, d.bt, st);
@@ -368,7 +303,8 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   }
   // split-K: raw slabs [batch][split][M][N], then ordered reduction + epilogue
   p.C = ws; p.ldc = d.N; p.sC = (long long)d.M * d.N;
-  hipError_t err = launch_layout<EPI_STORE>(p, d.at, d.bt, st);
+  hipError_t err = d.prec != GEMM_F32 ? gemm_bf16_launch(p, d.at, d.bt, d.prec, EPI_STORE, st)
+                                      : launch_store(p, d.at, d.bt, d.variant, st);
   if (err != hipSuccess) return err;
   const long long total = (long long)d.M * d.N;
   int grid = (int)std::min<long long>((total + 255) / 256, 2048);

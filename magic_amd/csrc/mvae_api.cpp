@@ -261,8 +261,9 @@ static int validate(const mvae_cfg* cfg) {
   if (cfg->act != MVAE_ACT_TANH && cfg->act != MVAE_ACT_ELU) return fail(nullptr, MVAE_ECONFIG, "bad act");
   if (cfg->metric != MVAE_METRIC_COSINE && cfg->metric != MVAE_METRIC_SQDIFF)
     return fail(nullptr, MVAE_ECONFIG, "bad metric");
-  if (cfg->precision != MVAE_PREC_F32)
-    return fail(nullptr, MVAE_ECONFIG, "precision: only MVAE_PREC_F32 is built in this library");
+  if (cfg->precision != MVAE_PREC_F32 && cfg->precision != MVAE_PREC_BF16 &&
+      cfg->precision != MVAE_PREC_F32X)
+    return fail(nullptr, MVAE_ECONFIG, "bad precision");
   const long long D = (long long)cfg->image_size * cfg->image_size;
   if (D * 3 * cfg->batch > (1LL << 31) - 1 || 3LL * cfg->batch * (D + 4) > (1LL << 31) * 8)
     return fail(nullptr, MVAE_ECONFIG, "batch too large for 32-bit row indexing");
@@ -394,6 +395,11 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     return (int)e;
   }
   build_schedule(c);
+  const int gp = cfg->precision == MVAE_PREC_BF16 ? GEMM_BF16
+                 : (cfg->precision == MVAE_PREC_F32X ? GEMM_F32X : GEMM_F32);
+  for (auto* v : {&c->fwd_enc, &c->bwd_dec, &c->bwd_enc})
+    for (auto& d : *v) d.prec = gp;
+  c->f_d1.prec = c->f_d2.prec = c->f_out.prec = gp;
   size_t ws = 0;
   for (auto& d : c->fwd_enc) ws = std::max(ws, gemm_workspace_elems(d));
   for (auto& d : c->bwd_dec) ws = std::max(ws, gemm_workspace_elems(d));
@@ -693,6 +699,7 @@ extern "C" int mvae_generate(mvae_ctx* ctx, const float* zin, int n, float* y_ou
   GemmDesc d2 = c->f_d2; d2.M = n;
   GemmDesc d3 = gd(n, c->D, c->d1 + 1, c->a2, c->ld_d2, false, c->theta + c->vo.off, c->D, false,
                    y_out, c->D, EPI_SIGMOID);
+  d3.prec = c->f_out.prec;
   int rc;
   if ((rc = run(c, d1, st))) return rc;
   if ((rc = run(c, d2, st))) return rc;
@@ -706,8 +713,10 @@ extern "C" int mvae_generate(mvae_ctx* ctx, const float* zin, int n, float* y_ou
 extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int at, const float* Bm,
                                int ldb, int bt, float* Cm, int ldc, int epi, int act, const float* aux,
                                int ld_aux, void* stream) {
-  if (epi == EPI_BCE || epi < 0 || epi > EPI_SIGMOID) return fail(nullptr, MVAE_EINVAL, "bad epilogue");
-  GemmDesc d = gd(M, N, K, A, lda, at != 0, Bm, ldb, bt != 0, Cm, ldc, epi);
+  if ((epi & 15) == EPI_BCE || epi < 0 || (epi & 15) > EPI_SIGMOID || (epi >> 4) > 2)
+    return fail(nullptr, MVAE_EINVAL, "bad epilogue");
+  GemmDesc d = gd(M, N, K, A, lda, at != 0, Bm, ldb, bt != 0, Cm, ldc, epi & 15);
+  d.prec = epi >> 4;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
   d.epi.act = act;
   d.epi.aux = aux;
   d.epi.ld_aux = ld_aux;
@@ -765,5 +774,44 @@ extern "C" int mvae_timing_reset(mvae_ctx* ctx) {
   if (rc) return rc;
   std::fill(ctx->region_ms.begin(), ctx->region_ms.end(), 0.0);
   std::fill(ctx->region_n.begin(), ctx->region_n.end(), 0);
+  return MVAE_OK;
+}
+
+// Time one GEMM shape of the step's kernel family (diagnostics): operands are allocated
+// and filled with uniform [-1,1) values inside, `iters` launches are timed with HIP events
+// on `stream` after 3 warm-ups. variant selects a kernel variant (0 = default).
+extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, int variant, int iters,
+                               void* stream, float* avg_ms) {
+  if (M <= 0 || N <= 0 || K <= 0 || iters <= 0 || !avg_ms || batch <= 0) return MVAE_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const size_t na = (size_t)M * K * batch, nb = (size_t)K * N * batch, nc = (size_t)M * N * batch;
+  float *A = nullptr, *Bm = nullptr, *Cm = nullptr, *ws = nullptr;
+  GemmDesc d = gd(M, N, K, nullptr, at ? M : K, at != 0, nullptr, bt ? K : N, bt != 0, nullptr, N);
+  d.batch = batch; d.sA = (long long)M * K; d.sB = (long long)K * N; d.sC = (long long)M * N;
+  d.variant = variant & 15;
+  d.prec = variant >> 4;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
+  const size_t ws_n = gemm_workspace_elems(d);
+  hipError_t e = hipMalloc(&A, na * 4);
+  if (e == hipSuccess) e = hipMalloc(&Bm, nb * 4);
+  if (e == hipSuccess) e = hipMalloc(&Cm, nc * 4);
+  if (e == hipSuccess && ws_n) e = hipMalloc(&ws, ws_n * 4);
+  if (e == hipSuccess) e = launch_normal(A, na, 1, 0, st);
+  if (e == hipSuccess) e = launch_normal(Bm, nb, 2, 0, st);
+  d.A = A; d.B = Bm; d.C = Cm;
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  if (e == hipSuccess) e = hipEventCreate(&t0);
+  if (e == hipSuccess) e = hipEventCreate(&t1);
+  for (int i = 0; e == hipSuccess && i < 3; ++i) e = gemm_run(d, ws, ws_n, st);
+  if (e == hipSuccess) e = hipEventRecord(t0, st);
+  for (int i = 0; e == hipSuccess && i < iters; ++i) e = gemm_run(d, ws, ws_n, st);
+  if (e == hipSuccess) e = hipEventRecord(t1, st);
+  if (e == hipSuccess) e = hipEventSynchronize(t1);
+  float ms = 0.f;
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, t0, t1);
+  *avg_ms = ms / iters;
+  if (t0) (void)hipEventDestroy(t0);
+  if (t1) (void)hipEventDestroy(t1);
+  for (float* p : {A, Bm, Cm, ws}) if (p) (void)hipFree(p);
+  if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
   return MVAE_OK;
 }

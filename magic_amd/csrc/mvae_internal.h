@@ -17,6 +17,10 @@ enum EpiMode {
 
 enum Act { ACT_TANH = 0, ACT_ELU = 1 };
 
+// GEMM arithmetic: native fp32 MFMA; bf16 operands (fp32 accumulate); fp32-accurate
+// 3-term exact bf16 split (see gemm_bf16.hip).
+enum GemmPrec { GEMM_F32 = 0, GEMM_BF16 = 1, GEMM_F32X = 2 };
+
 struct GemmEpi {
   int mode = EPI_STORE;
   int act = ACT_TANH;
@@ -43,6 +47,9 @@ struct GemmDesc {
   const __hip_bfloat16* Ah = nullptr;  // bf16 shadows (nullptr = fp32 operands)
   const __hip_bfloat16* Bh = nullptr;
   __hip_bfloat16* Ch = nullptr;        // optional bf16 copy of the epilogue output (ldc)
+  int prec = GEMM_F32;                 // GemmPrec
+  int variant = 0;                     // kernel variant (diagnostics / A-B); 0 = default
+  int split = 0;                       // forced split-K (0 = planner)
   GemmEpi epi;
 };
 
@@ -52,6 +59,8 @@ int gemm_plan_split(const GemmDesc& d, size_t max_ws);
 size_t gemm_workspace_elems(const GemmDesc& d);
 // Launch. ws: device workspace of >= gemm_workspace_elems(d) floats.
 hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t st);
+namespace gemm { struct Params; }
+hipError_t gemm_bf16_launch(const gemm::Params& p, bool at, bool bt, int mode, int epi, hipStream_t st);
 // Number of column blocks the BCE epilogue writes per row (rowpart's inner dim).
 int gemm_bce_nblk(int N);
 

@@ -133,8 +133,9 @@ def act_grad(y, g, kind):
 
 
 def split_input(X, cfg):
-    """``11a/vae.py:172-185``: reshape [B,H,W,3] + split(axis=3): channel c at (h*W+w)*3+c."""
-    return X[:, 0::3], X[:, 1::3], X[:, 2::3]
+    """``11a/vae.py:172-185``: reshape [B,H,W,3] + split(axis=3): channel c at (h*W+w)*3+c.
+    Contiguous copies, so the matmuls run in BLAS (strided operands fall off the BLAS path)."""
+    return tuple(np.ascontiguousarray(X[:, c::3]) for c in range(3))
 
 
 def encode(P, x, cfg):
@@ -305,12 +306,14 @@ def backward(c, cfg, B_global: int, coldot_global=None, magnitude: bool = False)
 
 
 # --------------------------------------------------------------------------- Adam
-def adam_init(cfg, P) -> dict:
+def adam_init(cfg, P, dtype=None) -> dict:
+    """Slots in ``dtype`` (default: float64 for float64 parameters, else float32)."""
     f32 = np.float32
     st = {"t": 0}
     for o, names in ((1, trained_names(cfg)), (2, encoder_names(cfg))):
-        st[f"m{o}"] = {n: np.zeros_like(P[n], dtype=np.float64) for n in names}
-        st[f"v{o}"] = {n: np.zeros_like(P[n], dtype=np.float64) for n in names}
+        dt = dtype or (np.float64 if P[names[0]].dtype == np.float64 else np.float32)
+        st[f"m{o}"] = {n: np.zeros_like(P[n], dtype=dt) for n in names}
+        st[f"v{o}"] = {n: np.zeros_like(P[n], dtype=dt) for n in names}
         st[f"b1p{o}"] = f32(cfg.beta1)
         st[f"b2p{o}"] = f32(cfg.beta2)
     return st
@@ -329,9 +332,10 @@ def adam(P, g1, g2, st, cfg, dtype=np.float64):
     for o, g in ((1, g1), (2, g2)):
         lr_t = float(adam_lr_t(cfg.lr[o - 1], st[f"b1p{o}"], st[f"b2p{o}"]))
         for n, gn in g.items():
-            m = st[f"m{o}"][n] = st[f"m{o}"][n] + (gn - st[f"m{o}"][n]) * (1 - b1)
-            v = st[f"v{o}"][n] = st[f"v{o}"][n] + (gn * gn - st[f"v{o}"][n]) * (1 - b2)
-            P[n] = P[n] - (lr_t * m) / (np.sqrt(v) + e)
+            sd = st[f"m{o}"][n].dtype
+            m = st[f"m{o}"][n] = (st[f"m{o}"][n] + (gn - st[f"m{o}"][n]) * (1 - b1)).astype(sd, copy=False)
+            v = st[f"v{o}"][n] = (st[f"v{o}"][n] + (gn * gn - st[f"v{o}"][n]) * (1 - b2)).astype(sd, copy=False)
+            P[n] = (P[n] - (lr_t * m) / (np.sqrt(v) + e)).astype(dtype, copy=False)
         st[f"b1p{o}"] = np.float32(st[f"b1p{o}"] * np.float32(b1))
         st[f"b2p{o}"] = np.float32(st[f"b2p{o}"] * np.float32(b2))
     st["t"] += 1

@@ -1,0 +1,70 @@
+#!/usr/bin/env python3
+"""A/B the GEMM kernel variants on the training step's shapes, interleaved rounds in ONE
+process (cdna_hip_programming.md §5.4 rule 24). Prints TFLOP/s per (shape, variant).
+
+  python tools/gemm_bench.py [--variants 0,1,2] [--rounds 3] [--config C2]
+"""
+import argparse
+import ctypes as C
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from magic_amd import _lib  # noqa: E402
+from magic_amd.config import baseline_config  # noqa: E402
+
+
+def shapes(cfg):
+    B, D, e, L = cfg.batch, cfg.D, cfg.enc[0], cfg.latent
+    d1 = cfg.dec[1]
+    return [
+        ("enc_fwd_0", 3 * B, e, D + 1, 0, 0, 1),
+        ("enc_bwd_w_0", D + 1, e, 2 * B, 1, 0, 2),
+        ("dec_fwd_out", B, D, d1 + 1, 0, 0, 1),
+        ("dec_bwd_d_out", B, d1, D, 0, 1, 1),
+        ("dec_bwd_w_out", d1 + 1, D, B, 1, 0, 1),
+        ("enc_fwd_h", 3 * B, e, e + 1, 0, 0, 1),
+        ("enc_bwd_d_h", 4 * B, e, e, 0, 1, 1),
+        ("enc_bwd_w_h", e + 1, e, 2 * B, 1, 0, 2),
+        ("head_fwd", 3 * B, 2 * L, e + 1, 0, 0, 1),
+        ("square4096", 4096, 4096, 4096, 0, 0, 1),
+    ]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0,16,32")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--config", default="C2")
+    args = ap.parse_args()
+    lib = _lib.load()
+    torch.cuda.init()
+    st = torch.cuda.current_stream().cuda_stream
+    cfg = baseline_config(args.config)
+    variants = [int(v) for v in args.variants.split(",")]
+    res = {}
+    for _ in range(args.rounds):
+        for name, M, N, K, at, bt, batch in shapes(cfg):
+            for v in variants:
+                ms = C.c_float()
+                rc = lib.mvae_bench_gemm(M, N, K, at, bt, batch, v, args.iters, st, C.byref(ms))
+                if rc != 0:
+                    raise RuntimeError(lib.mvae_last_error(None))
+                res.setdefault((name, v), []).append(ms.value)
+    print(f"{'shape':16s} {'MxNxK':>22s} batch " + " ".join(f"{'v' + str(v) + ' TF/s':>10s}" for v in variants))
+    for name, M, N, K, at, bt, batch in shapes(cfg):
+        fl = 2.0 * M * N * K * batch
+        cells = []
+        for v in variants:
+            med = statistics.median(res[(name, v)])
+            cells.append(f"{fl / med / 1e9:10.1f}")
+        print(f"{name:16s} {f'{M}x{N}x{K}':>22s} {batch:5d} " + " ".join(cells))
+
+
+if __name__ == "__main__":
+    main()
