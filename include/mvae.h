@@ -108,7 +108,8 @@ int mvae_buffer(mvae_ctx* ctx, int which, float** ptr, size_t* count);
 /* Optimizer step counters (TF beta1_power/beta2_power, kept on the host in fp32). */
 int mvae_get_step(mvae_ctx* ctx, int64_t* t1, int64_t* t2);
 int mvae_set_step(mvae_ctx* ctx, int64_t t1, int64_t t2);
-/* Re-derive the bf16 shadow weights from the fp32 masters (after an external write). */
+/* Re-derive the bf16 plane images of the parameters from the fp32 masters: call after
+ * writing parameters through mvae_param_info views (bf16 / f32x modes; no-op for f32). */
 int mvae_sync_params(mvae_ctx* ctx, void* stream);
 
 /* ---- training step, phase by phase --------------------------------------------- */
@@ -133,6 +134,14 @@ int mvae_transform(mvae_ctx* ctx, const float* x, float* zmean_out, void* stream
 int mvae_reconstruct(mvae_ctx* ctx, const float* x, const float* eps, float* y_out, void* stream);
 /* z: [n, L] (n <= B) -> y: [n, D] */
 int mvae_generate(mvae_ctx* ctx, const float* z, int n, float* y_out, void* stream);
+
+/* ---- batch producer (11a/overlap_input.py:127-261) -------------------------------- */
+/* locks, keys: uint8 [n][H][W] (decoded PNGs, 0..255) on the device; idx: int [B] example
+ * of each row; coef: float [B][4] = (cos, sin, x_off, y_off) of each row's rotation
+ * (tf.contrib.image.rotate, computed on the host in fp32, 16-byte aligned).
+ * Writes x_out [B, H*W*3] float32: per pixel (lock, rotated lock, key) / 255.            */
+int mvae_make_batch(const unsigned char* locks, const unsigned char* keys, int height, int width,
+                    const int* idx, const float* coef, int batch, float* x_out, void* stream);
 
 /* ---- diagnostics ------------------------------------------------------------------ */
 /* HIP-event timing of named regions (one GEMM incl. its split-K reduction, or one

@@ -71,6 +71,8 @@ _SIGS = {
     "mvae_transform": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mvae_reconstruct": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mvae_generate": ([C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p], C.c_int),
+    "mvae_make_batch": ([C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
+                         C.c_void_p, C.c_void_p], C.c_int),
     "mvae_timing_enable": ([C.c_void_p, C.c_int], C.c_int),
     "mvae_timing_regions": ([C.c_void_p], C.c_int),
     "mvae_timing_name": ([C.c_void_p, C.c_int], C.c_char_p),

@@ -39,6 +39,17 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
+// v -> n bf16 planes (n = 1: round to nearest; n = 3: exact split, each residual exact)
+__device__ __forceinline__ void store_planes(unsigned short* cp, long long pc, int n, size_t idx,
+                                             float v) {
+  float r = v;
+  for (int t = 0; t < n; ++t) {
+    const unsigned short b = __builtin_bit_cast(unsigned short, __float2bfloat16(r));
+    cp[t * pc + idx] = b;
+    r -= __uint_as_float((unsigned)b << 16);
+  }
+}
+
 // logical tile of this workgroup
 struct Tile {
   int z, bi, si, m0, n0, nt, ks, ke;
@@ -72,6 +83,7 @@ __device__ __forceinline__ void epilogue(const Params& p, const Tile& t, f32x16 
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 31, fk = lane >> 5;
   float* __restrict__ C = p.C + (size_t)t.z * p.sC;  // z = bi*split + si (slab) or bi (split==1)
+  unsigned short* cp = p.epi.cp ? p.epi.cp + (size_t)t.z * p.sC : nullptr;
   const int rbase = t.m0 + wm * 64 + 4 * fk;
   const int cbase = t.n0 + wn * 64 + fr;
   if constexpr (EPI == EPI_BCE) {
@@ -93,7 +105,9 @@ __device__ __forceinline__ void epilogue(const Params& p, const Tile& t, f32x16 
             if (xv != 0.f) term += xv * logf(yv);
             if (xv != 1.f) term += (1.f - xv) * logf(1.f - yv);
             rs += term;
-            C[(size_t)row * p.ldc + col] = (yv - xv) * e.scale;
+            const float du = (yv - xv) * e.scale;
+            C[(size_t)row * p.ldc + col] = du;
+            if (cp) store_planes(cp, e.pc, e.ncp, (size_t)row * p.ldc + col, du);
             if (e.y) e.y[(size_t)row * e.ldy + col] = yv;
           }
         }
@@ -125,6 +139,7 @@ __device__ __forceinline__ void epilogue(const Params& p, const Tile& t, f32x16 
             v = dact_f(v, p.epi.aux[(size_t)ar * p.epi.ld_aux + col], p.epi.act);
           }
           C[(size_t)row * p.ldc + col] = v;
+          if (cp) store_planes(cp, p.epi.pc, p.epi.ncp, (size_t)row * p.ldc + col, v);
         }
       }
     }

@@ -217,6 +217,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, in
       v = dact_f(v, e.aux[(size_t)ar * e.ld_aux + col], e.act);
     }
     c[(size_t)row * ldc + col] = v;
+    if (e.cp) store_planes(e.cp + bi * sC, e.pc, e.ncp, (size_t)row * ldc + col, v);
   }
 }
 
@@ -291,7 +292,7 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   p.kchunk = ((ktiles + split - 1) / split) * BK;
   if (split == 1) {
     p.C = d.C; p.ldc = d.ldc; p.sC = d.sC;
-    if (d.prec != GEMM_F32) return gemm_bf16_launch(p, d.at, d.bt, d.prec, d.epi.mode, st);
+    if (d.prec != GEMM_F32) return gemm_bf16_launch(p, d, d.epi.mode, st);
     switch (d.epi.mode) {
       case EPI_STORE: return launch_store(p, d.at, d.bt, d.variant, st);
       case EPI_ACT: return launch_layout<EPI_ACT>(p, d.at, d.bt, st);
@@ -303,7 +304,8 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   }
   // split-K: raw slabs [batch][split][M][N], then ordered reduction + epilogue
   p.C = ws; p.ldc = d.N; p.sC = (long long)d.M * d.N;
-  hipError_t err = d.prec != GEMM_F32 ? gemm_bf16_launch(p, d.at, d.bt, d.prec, EPI_STORE, st)
+  p.epi.cp = nullptr;  // planes are written by the reduction
+  hipError_t err = d.prec != GEMM_F32 ? gemm_bf16_launch(p, d, EPI_STORE, st)
                                       : launch_store(p, d.at, d.bt, d.variant, st);
   if (err != hipSuccess) return err;
   const long long total = (long long)d.M * d.N;

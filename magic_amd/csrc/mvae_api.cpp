@@ -26,9 +26,10 @@ namespace {
 struct Block {
   size_t off = 0;  // element offset in theta / g1
   int K = 0, N = 0;
+  int ld = 0;      // row stride: N rounded up to 8 (16-B rows for the bf16 plane images)
 };
 
-inline int round4(int v) { return (v + 3) & ~3; }
+inline int round8(int v) { return (v + 7) & ~7; }
 inline size_t align64(size_t v) { return (v + 63) & ~size_t(63); }
 
 }  // namespace
@@ -38,7 +39,7 @@ struct mvae_ctx {
   int device = 0;
   int B = 0, D = 0, L = 0, nenc = 0, d0 = 0, d1 = 0;
   float inv_bg = 1.f;
-  int ldx = 0, ldz = 0, ld_d1 = 0, ld_d2 = 0, ld_u = 0, lddz = 0, nblk = 0, nchunk = 0;
+  int ldx = 0, ldz = 0, ld_d1 = 0, ld_d2 = 0, ld_u = 0, lddz = 0, ld_dh = 0, nblk = 0, nchunk = 0;
   std::vector<int> ldh;
   // parameters
   std::vector<Block> enc;
@@ -59,6 +60,11 @@ struct mvae_ctx {
   float* ws = nullptr;
   size_t ws_elems = 0;
   std::vector<void*> allocs;
+  // bf16 plane images (bf16 / f32x modes): fp32 buffer -> planes of the same layout
+  struct PlaneBuf { float* base; size_t n; Planes pl; };
+  std::vector<PlaneBuf> planes;
+  int np = 0;            // planes per buffer: 0 (fp32 mode), 1 (bf16), 3 (f32x)
+  int* dyn = nullptr;    // f32x: residual planes of the de-interleaved pixels nonzero?
   // schedule (each GEMM tagged with its timing region)
   std::vector<GemmDesc> fwd_enc;  // encoder layers + head
   GemmDesc f_d1, f_d2, f_out;
@@ -111,6 +117,16 @@ static hipError_t ones_column(float* base, int ld, int col, int rows) {
   std::vector<float> one(rows, 1.f);
   return hipMemcpy2D(base + col, (size_t)ld * sizeof(float), one.data(), sizeof(float), sizeof(float),
                      rows, hipMemcpyHostToDevice);
+}
+
+static Planes planes_of(const mvae_ctx* c, const float* p) {
+  for (const auto& b : c->planes)
+    if (p >= b.base && p < b.base + b.n) {
+      Planes r = b.pl;
+      r.p += (p - b.base);
+      return r;
+    }
+  return Planes{};
 }
 
 static GemmDesc gd(int M, int N, int K, const float* A, int lda, bool at, const float* Bm, int ldb,
@@ -167,13 +183,13 @@ static void build_schedule(mvae_ctx* c) {
     const float* A = i == 0 ? c->xs : c->H[i - 1];
     const int lda = i == 0 ? c->ldx : c->ldh[i - 1];
     GemmDesc d = gd(3 * B, c->enc[i].N, c->enc[i].K + 1, A, lda, false, th + c->enc[i].off,
-                    c->enc[i].N, false, c->H[i], c->ldh[i], EPI_ACT);
+                    c->enc[i].ld, false, c->H[i], c->ldh[i], EPI_ACT);
     d.epi.act = act;
     c->fwd_enc.push_back(d);
     c->fwd_enc_r.push_back(region(c, "enc_fwd_" + std::to_string(i)));
   }
   c->fwd_enc.push_back(gd(3 * B, 2 * L, c->head.K + 1, c->H[n - 1], c->ldh[n - 1], false,
-                          th + c->head.off, 2 * L, false, c->ms, 2 * L));
+                          th + c->head.off, c->head.ld, false, c->ms, 2 * L));
   c->fwd_enc_r.push_back(region(c, "head_fwd"));
   c->f_d1_r = region(c, "dec_fwd_1");
   c->f_d2_r = region(c, "dec_fwd_2");
@@ -182,13 +198,13 @@ static void build_schedule(mvae_ctx* c) {
                          "dec_bwd_d_z"})
     c->bwd_dec_r.push_back(region(c, nm));
   // ---- decoder on the lock rows
-  c->f_d1 = gd(B, c->d0, L + 1, c->z + (size_t)B * c->ldz, c->ldz, false, th + c->v1.off, c->d0,
+  c->f_d1 = gd(B, c->d0, L + 1, c->z + (size_t)B * c->ldz, c->ldz, false, th + c->v1.off, c->v1.ld,
                false, c->a1, c->ld_d1, EPI_ACT);
   c->f_d1.epi.act = act;
-  c->f_d2 = gd(B, c->d1, c->d0 + 1, c->a1, c->ld_d1, false, th + c->v2.off, c->d1, false, c->a2,
+  c->f_d2 = gd(B, c->d1, c->d0 + 1, c->a1, c->ld_d1, false, th + c->v2.off, c->v2.ld, false, c->a2,
                c->ld_d2, EPI_ACT);
   c->f_d2.epi.act = act;
-  c->f_out = gd(B, c->D, c->d1 + 1, c->a2, c->ld_d2, false, th + c->vo.off, c->D, false, c->du,
+  c->f_out = gd(B, c->D, c->d1 + 1, c->a2, c->ld_d2, false, th + c->vo.off, c->vo.ld, false, c->du,
                 c->ld_u, EPI_BCE);
   c->f_out.epi.x = c->xs + (size_t)B * c->ldx;
   c->f_out.epi.ldx = c->ldx;
@@ -197,30 +213,30 @@ static void build_schedule(mvae_ctx* c) {
   // ---- decoder backward (g1 only)
   c->bwd_dec.clear();
   c->bwd_dec.push_back(gd(c->d1 + 1, c->D, B, c->a2, c->ld_d2, true, c->du, c->ld_u, false,
-                          g1 + c->vo.off, c->D));
-  GemmDesc dout = gd(B, c->d1, c->D, c->du, c->ld_u, false, th + c->vo.off, c->D, true, c->dzd2,
+                          g1 + c->vo.off, c->vo.ld));
+  GemmDesc dout = gd(B, c->d1, c->D, c->du, c->ld_u, false, th + c->vo.off, c->vo.ld, true, c->dzd2,
                      c->ld_d2, EPI_DACT);
   dout.epi.act = act; dout.epi.aux = c->a2; dout.epi.ld_aux = c->ld_d2;
   c->bwd_dec.push_back(dout);
   c->bwd_dec.push_back(gd(c->d0 + 1, c->d1, B, c->a1, c->ld_d1, true, c->dzd2, c->ld_d2, false,
-                          g1 + c->v2.off, c->d1));
-  GemmDesc dd2 = gd(B, c->d0, c->d1, c->dzd2, c->ld_d2, false, th + c->v2.off, c->d1, true, c->dzd1,
+                          g1 + c->v2.off, c->v2.ld));
+  GemmDesc dd2 = gd(B, c->d0, c->d1, c->dzd2, c->ld_d2, false, th + c->v2.off, c->v2.ld, true, c->dzd1,
                     c->ld_d1, EPI_DACT);
   dd2.epi.act = act; dd2.epi.aux = c->a1; dd2.epi.ld_aux = c->ld_d1;
   c->bwd_dec.push_back(dd2);
   c->bwd_dec.push_back(gd(L + 1, c->d0, B, c->z + (size_t)B * c->ldz, c->ldz, true, c->dzd1,
-                          c->ld_d1, false, g1 + c->v1.off, c->d0));
-  c->bwd_dec.push_back(gd(B, L, c->d0, c->dzd1, c->ld_d1, false, th + c->v1.off, c->d0, true,
+                          c->ld_d1, false, g1 + c->v1.off, c->v1.ld));
+  c->bwd_dec.push_back(gd(B, L, c->d0, c->dzd1, c->ld_d1, false, th + c->v1.off, c->v1.ld, true,
                           c->dzdec, L));
   // ---- encoder backward: g1 over rows [rot|lock], g2 over [lock|key] (batched GEMMs)
   c->bwd_enc.clear();
   {
-    GemmDesc w = gd(c->head.K + 1, 2 * L, 2 * B, c->H[n - 1], c->ldh[n - 1], true, c->dhead, 2 * L,
-                    false, g1 + c->head.off, 2 * L);
-    w.batch = 2; w.sA = (long long)B * c->ldh[n - 1]; w.sB = (long long)2 * B * 2 * L; w.sC = n_all;
+    GemmDesc w = gd(c->head.K + 1, 2 * L, 2 * B, c->H[n - 1], c->ldh[n - 1], true, c->dhead, c->ld_dh,
+                    false, g1 + c->head.off, c->head.ld);
+    w.batch = 2; w.sA = (long long)B * c->ldh[n - 1]; w.sB = (long long)2 * B * c->ld_dh; w.sC = n_all;
     c->bwd_enc.push_back(w);
     c->bwd_enc_r.push_back(region(c, "head_bwd_w"));
-    GemmDesc d = gd(4 * B, c->head.K, 2 * L, c->dhead, 2 * L, false, th + c->head.off, 2 * L, true,
+    GemmDesc d = gd(4 * B, c->head.K, 2 * L, c->dhead, c->ld_dh, false, th + c->head.off, c->head.ld, true,
                     c->dz[(n - 1) & 1], c->lddz, EPI_DACT);
     d.epi.act = act; d.epi.aux = c->H[n - 1]; d.epi.ld_aux = c->ldh[n - 1];
     d.epi.remap_split = 2 * B; d.epi.remap_shift = B;
@@ -231,13 +247,13 @@ static void build_schedule(mvae_ctx* c) {
     const float* A = i == 0 ? c->xs : c->H[i - 1];
     const int lda = i == 0 ? c->ldx : c->ldh[i - 1];
     GemmDesc w = gd(c->enc[i].K + 1, c->enc[i].N, 2 * B, A, lda, true, c->dz[i & 1], c->lddz, false,
-                    g1 + c->enc[i].off, c->enc[i].N);
+                    g1 + c->enc[i].off, c->enc[i].ld);
     w.batch = 2; w.sA = (long long)B * lda; w.sB = (long long)2 * B * c->lddz; w.sC = n_all;
     c->bwd_enc.push_back(w);
     c->bwd_enc_r.push_back(region(c, "enc_bwd_w_" + std::to_string(i)));
     if (i > 0) {
       GemmDesc d = gd(4 * B, c->enc[i].K, c->enc[i].N, c->dz[i & 1], c->lddz, false,
-                      th + c->enc[i].off, c->enc[i].N, true, c->dz[(i - 1) & 1], c->lddz, EPI_DACT);
+                      th + c->enc[i].off, c->enc[i].ld, true, c->dz[(i - 1) & 1], c->lddz, EPI_DACT);
       d.epi.act = act; d.epi.aux = c->H[i - 1]; d.epi.ld_aux = c->ldh[i - 1];
       d.epi.remap_split = 2 * B; d.epi.remap_shift = B;
       c->bwd_enc.push_back(d);
@@ -315,33 +331,34 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   size_t off = 0;
   int fan_in = c->D;
   for (int i = 0; i < c->nenc; ++i) {
-    Block b; b.off = off; b.K = fan_in; b.N = cfg->enc[i];
+    Block b; b.off = off; b.K = fan_in; b.N = cfg->enc[i]; b.ld = round8(b.N);
     c->enc.push_back(b);
-    off = align64(off + (size_t)(b.K + 1) * b.N);
+    off = align64(off + (size_t)(b.K + 1) * b.ld);
     fan_in = b.N;
   }
-  c->head.off = off; c->head.K = fan_in; c->head.N = 2 * c->L;
-  off = align64(off + (size_t)(fan_in + 1) * 2 * c->L);
+  c->head.off = off; c->head.K = fan_in; c->head.N = 2 * c->L; c->head.ld = round8(2 * c->L);
+  off = align64(off + (size_t)(fan_in + 1) * c->head.ld);
   c->n_enc = off;
-  c->v1.off = off; c->v1.K = c->L; c->v1.N = c->d0;
-  off = align64(off + (size_t)(c->L + 1) * c->d0);
-  c->v2.off = off; c->v2.K = c->d0; c->v2.N = c->d1;
-  off = align64(off + (size_t)(c->d0 + 1) * c->d1);
-  c->vo.off = off; c->vo.K = c->d1; c->vo.N = c->D;
-  off = align64(off + (size_t)(c->d1 + 1) * c->D);
+  c->v1.off = off; c->v1.K = c->L; c->v1.N = c->d0; c->v1.ld = round8(c->d0);
+  off = align64(off + (size_t)(c->L + 1) * c->v1.ld);
+  c->v2.off = off; c->v2.K = c->d0; c->v2.N = c->d1; c->v2.ld = round8(c->d1);
+  off = align64(off + (size_t)(c->d0 + 1) * c->v2.ld);
+  c->vo.off = off; c->vo.K = c->d1; c->vo.N = c->D; c->vo.ld = round8(c->D);
+  off = align64(off + (size_t)(c->d1 + 1) * c->vo.ld);
   c->n_all = off;
   // ---- strides
-  c->ldx = round4(c->D + 1);
-  c->ldz = round4(c->L + 1);
-  c->ld_d1 = round4(c->d0 + 1);
-  c->ld_d2 = round4(c->d1 + 1);
-  c->ld_u = round4(c->D);
+  c->ldx = round8(c->D + 1);
+  c->ldz = round8(c->L + 1);
+  c->ld_d1 = round8(c->d0 + 1);
+  c->ld_d2 = round8(c->d1 + 1);
+  c->ld_u = round8(c->D);
+  c->ld_dh = round8(2 * c->L);
   int maxe = 0;
   for (int i = 0; i < c->nenc; ++i) {
-    c->ldh.push_back(round4(cfg->enc[i] + 1));
+    c->ldh.push_back(round8(cfg->enc[i] + 1));
     maxe = std::max(maxe, cfg->enc[i]);
   }
-  c->lddz = round4(maxe);
+  c->lddz = round8(maxe);
   c->nblk = gemm_bce_nblk(c->D);
   c->nchunk = colstats_nchunk(c->B);
   const size_t B = c->B, L = c->L;
@@ -379,7 +396,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   ALLOC(c->dzd2, B * c->ld_d2);
   ALLOC(c->dzd1, B * c->ld_d1);
   ALLOC(c->dzdec, B * L);
-  ALLOC(c->dhead, 4 * B * 2 * L);
+  ALLOC(c->dhead, 4 * B * c->ld_dh);
   ALLOC(c->dz[0], 4 * B * c->lddz);
   ALLOC(c->dz[1], 4 * B * c->lddz);
   // constant ones columns (bias folding)
@@ -397,9 +414,61 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   build_schedule(c);
   const int gp = cfg->precision == MVAE_PREC_BF16 ? GEMM_BF16
                  : (cfg->precision == MVAE_PREC_F32X ? GEMM_F32X : GEMM_F32);
+  c->np = gp == GEMM_BF16 ? 1 : (gp == GEMM_F32X ? 3 : 0);
+  if (c->np) {
+    // plane images of every GEMM operand buffer (filled from the fp32 buffer once here,
+    // then written by each producer: de-interleave, epilogues, latent kernels, Adam)
+    auto add = [&](float* base, size_t n) -> hipError_t {
+      void* q = nullptr;
+      hipError_t e = hipMalloc(&q, (size_t)c->np * n * sizeof(unsigned short));
+      if (e != hipSuccess) return e;
+      c->allocs.push_back(q);
+      mvae_ctx::PlaneBuf pb{base, n, Planes{static_cast<unsigned short*>(q), (long long)n, c->np}};
+      c->planes.push_back(pb);
+      return launch_split_planes(base, n, pb.pl, nullptr);
+    };
+    hipError_t e = add(c->theta, c->n_all);
+    if (e == hipSuccess) e = add(c->xs, 3 * B * c->ldx);
+    for (int i = 0; e == hipSuccess && i < c->nenc; ++i) e = add(c->H[i], 3 * B * c->ldh[i]);
+    if (e == hipSuccess) e = add(c->z, 3 * B * c->ldz);
+    if (e == hipSuccess) e = add(c->zgen, B * c->ldz);
+    if (e == hipSuccess) e = add(c->a1, B * c->ld_d1);
+    if (e == hipSuccess) e = add(c->a2, B * c->ld_d2);
+    if (e == hipSuccess) e = add(c->du, B * c->ld_u);
+    if (e == hipSuccess) e = add(c->dzd2, B * c->ld_d2);
+    if (e == hipSuccess) e = add(c->dzd1, B * c->ld_d1);
+    if (e == hipSuccess) e = add(c->dhead, 4 * B * c->ld_dh);
+    if (e == hipSuccess) e = add(c->dz[0], 4 * B * c->lddz);
+    if (e == hipSuccess) e = add(c->dz[1], 4 * B * c->lddz);
+    if (e == hipSuccess && c->np == 3) e = dalloc(c, reinterpret_cast<float**>(&c->dyn), 4);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+      g_create_err = std::string("plane images: ") + hipGetErrorString(e);
+      mvae_destroy(c);
+      return (int)e;
+    }
+  }
+  auto wire = [&](GemmDesc& d) {
+    d.prec = gp;
+    if (!c->np) return;
+    const Planes a = planes_of(c, d.A), b = planes_of(c, d.B), o = planes_of(c, d.C);
+    d.Ap = a.p; d.pA = a.stride; d.nA = c->np;
+    d.Bp = b.p; d.pB = b.stride; d.nB = c->np;
+    d.epi.cp = o.p; d.epi.pc = o.stride; d.epi.ncp = o.p ? c->np : 0;
+    d.dynA = (c->dyn && d.A >= c->xs && d.A < c->xs + (size_t)3 * B * c->ldx) ? c->dyn : nullptr;
+  };
   for (auto* v : {&c->fwd_enc, &c->bwd_dec, &c->bwd_enc})
-    for (auto& d : *v) d.prec = gp;
-  c->f_d1.prec = c->f_d2.prec = c->f_out.prec = gp;
+    for (auto& d : *v) wire(d);
+  wire(c->f_d1);
+  wire(c->f_d2);
+  wire(c->f_out);
+  for (auto* v : {&c->fwd_enc, &c->bwd_dec, &c->bwd_enc})
+    for (auto& d : *v)
+      if (c->np && (!d.Ap || !d.Bp)) {
+        g_create_err = "internal: GEMM operand without plane image";
+        mvae_destroy(c);
+        return MVAE_EINVAL;
+      }
   size_t ws = 0;
   for (auto& d : c->fwd_enc) ws = std::max(ws, gemm_workspace_elems(d));
   for (auto& d : c->bwd_dec) ws = std::max(ws, gemm_workspace_elems(d));
@@ -431,14 +500,14 @@ int mvae_param_info(mvae_ctx* ctx, int kind, int index, mvae_tensor* out) {
     bias = index & 1;
     blk = &ctx->enc[i];
     name = "enc_h" + std::to_string(i) + (bias ? "_b" : "_W");
-    cols = blk->N; ld = blk->N; enc_part = 1;
+    cols = blk->N; ld = blk->ld; enc_part = 1;
   } else if (index < 2 * n + 4) {
     const int j = index - 2 * n;
     blk = &ctx->head;
     bias = j & 1;
     const bool logsig = j >= 2;
     name = std::string(logsig ? "enc_out_log_sigma" : "enc_out_mean") + (bias ? "_b" : "_W");
-    col0 = logsig ? ctx->L : 0; cols = ctx->L; ld = 2 * ctx->L; enc_part = 1;
+    col0 = logsig ? ctx->L : 0; cols = ctx->L; ld = blk->ld; enc_part = 1;
   } else if (index < 2 * n + 10) {
     const int j = index - 2 * n - 4;
     const Block* bl[3] = {&ctx->v1, &ctx->v2, &ctx->vo};
@@ -446,7 +515,7 @@ int mvae_param_info(mvae_ctx* ctx, int kind, int index, mvae_tensor* out) {
     blk = bl[j / 2];
     bias = j & 1;
     name = std::string(nm[j / 2]) + (bias ? "_b" : "_W");
-    cols = blk->N; ld = blk->N;
+    cols = blk->N; ld = blk->ld;
   } else {  // dead decoder log-sigma variables (11a/vae.py:147,153): allocated, never trained
     bias = (index - 2 * n - 10) == 1;
     std::strncpy(out->name, bias ? "dec_out_log_sigma_b" : "dec_out_log_sigma_W", sizeof(out->name) - 1);
@@ -517,8 +586,9 @@ int mvae_set_step(mvae_ctx* ctx, int64_t t1, int64_t t2) {
 }
 
 int mvae_sync_params(mvae_ctx* ctx, void* stream) {
-  (void)stream;
-  return ctx ? MVAE_OK : MVAE_EINVAL;  // fp32 build: no shadows to refresh
+  if (!ctx) return MVAE_EINVAL;
+  MV_CHECK(launch_split_planes(ctx->theta, ctx->n_all, planes_of(ctx, ctx->theta), (hipStream_t)stream));
+  return MVAE_OK;
 }
 
 // ------------------------------------------------------------------ phases
@@ -533,7 +603,8 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
   auto c = ctx;
   {
     TIMED("deinterleave");
-    MV_CHECK(launch_deinterleave(x, c->xs, nullptr, c->B, c->D, c->ldx, st));
+    if (c->dyn) MV_CHECK(hipMemsetAsync(c->dyn, 0, sizeof(int), st));
+    MV_CHECK(launch_deinterleave(x, c->xs, planes_of(c, c->xs), c->dyn, c->B, c->D, c->ldx, st));
   }
   const size_t ne = (size_t)3 * c->B * c->L;
   {
@@ -550,7 +621,7 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
   }
   {
     TIMED("latent_fwd");
-    MV_CHECK(launch_latent_fwd(c->ms, c->eps, c->z, nullptr, c->B, c->L, c->ldz, st));
+    MV_CHECK(launch_latent_fwd(c->ms, c->eps, c->z, planes_of(c, c->z), c->B, c->L, c->ldz, st));
   }
   if (c->cfg.metric == MVAE_METRIC_COSINE) {
     TIMED("colsq");
@@ -605,7 +676,7 @@ extern "C" int mvae_backward(mvae_ctx* ctx, void* stream) {
     TIMED("latent_bwd");
     MV_CHECK(launch_latent_bwd(c->z, c->ldz, c->ms, c->eps, c->dzdec, c->draw, c->colsq, c->coldot,
                                c->B, c->L, c->cfg.metric, c->cfg.deform_weight, c->inv_bg, c->dhead,
-                               nullptr, st));
+                               c->ld_dh, planes_of(c, c->dhead), st));
   }
   for (size_t i = 0; i < c->bwd_enc.size(); ++i)
     if ((rc = run(c, c->bwd_enc[i], st, c->bwd_enc_r[i]))) return rc;
@@ -626,7 +697,7 @@ extern "C" int mvae_adam(mvae_ctx* ctx, void* stream) {
   // TF ApplyAdam: lr_t = lr * sqrt(1 - beta2_power) / (1 - beta1_power), all fp32
   a.lr1 = (c->cfg.lr[0] * std::sqrt(1.f - c->b2p[0])) / (1.f - c->b1p[0]);
   a.lr2 = (c->cfg.lr[1] * std::sqrt(1.f - c->b2p[1])) / (1.f - c->b1p[1]);
-  a.theta_h = nullptr;
+  a.tp = planes_of(c, c->theta);
   hipStream_t st = (hipStream_t)stream;
   {
     TIMED("adam");
@@ -695,11 +766,12 @@ extern "C" int mvae_generate(mvae_ctx* ctx, const float* zin, int n, float* y_ou
   hipStream_t st = (hipStream_t)stream;
   auto c = ctx;
   MV_CHECK(launch_copy2d(zin, c->L, c->zgen, c->ldz, n, c->L, st));
+  MV_CHECK(launch_split_planes(c->zgen, (size_t)n * c->ldz, planes_of(c, c->zgen), st));
   GemmDesc d1 = c->f_d1; d1.M = n; d1.A = c->zgen;
+  { const Planes zp = planes_of(c, c->zgen); d1.Ap = zp.p; }
   GemmDesc d2 = c->f_d2; d2.M = n;
-  GemmDesc d3 = gd(n, c->D, c->d1 + 1, c->a2, c->ld_d2, false, c->theta + c->vo.off, c->D, false,
-                   y_out, c->D, EPI_SIGMOID);
-  d3.prec = c->f_out.prec;
+  GemmDesc d3 = c->f_out;
+  d3.M = n; d3.C = y_out; d3.ldc = c->D; d3.epi = GemmEpi(); d3.epi.mode = EPI_SIGMOID;
   int rc;
   if ((rc = run(c, d1, st))) return rc;
   if ((rc = run(c, d2, st))) return rc;
@@ -715,17 +787,34 @@ extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int
                                int ld_aux, void* stream) {
   if ((epi & 15) == EPI_BCE || epi < 0 || (epi & 15) > EPI_SIGMOID || (epi >> 4) > 2)
     return fail(nullptr, MVAE_EINVAL, "bad epilogue");
+  hipStream_t st = (hipStream_t)stream;
   GemmDesc d = gd(M, N, K, A, lda, at != 0, Bm, ldb, bt != 0, Cm, ldc, epi & 15);
   d.prec = epi >> 4;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
   d.epi.act = act;
   d.epi.aux = aux;
   d.epi.ld_aux = ld_aux;
+  std::vector<void*> tmp;
+  hipError_t e = hipSuccess;
+  if (d.prec != GEMM_F32) {  // plane images of the operands (the step's producers write these)
+    const int np = d.prec == GEMM_BF16 ? 1 : 3;
+    const size_t na = (size_t)(at ? K : M) * lda, nb = (size_t)(bt ? N : K) * ldb;
+    void *pa = nullptr, *pb = nullptr;
+    e = hipMalloc(&pa, np * na * 2);
+    if (e == hipSuccess) e = hipMalloc(&pb, np * nb * 2);
+    tmp = {pa, pb};
+    Planes A_{(unsigned short*)pa, (long long)na, np}, B_{(unsigned short*)pb, (long long)nb, np};
+    if (e == hipSuccess) e = launch_split_planes(A, na, A_, st);
+    if (e == hipSuccess) e = launch_split_planes(Bm, nb, B_, st);
+    d.Ap = A_.p; d.pA = A_.stride; d.nA = np;
+    d.Bp = B_.p; d.pB = B_.stride; d.nB = np;
+  }
   const size_t ws_n = gemm_workspace_elems(d);
   float* ws = nullptr;
-  if (ws_n && hipMalloc(&ws, ws_n * sizeof(float)) != hipSuccess) return fail(nullptr, MVAE_EINVAL, "ws alloc");
-  hipError_t e = gemm_run(d, ws, ws_n, (hipStream_t)stream);
-  if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+  if (e == hipSuccess && ws_n) e = hipMalloc(&ws, ws_n * sizeof(float));
+  if (e == hipSuccess) e = gemm_run(d, ws, ws_n, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (ws) (void)hipFree(ws);
+  for (void* q : tmp) if (q) (void)hipFree(q);
   if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
   return MVAE_OK;
 }
@@ -790,14 +879,24 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   d.batch = batch; d.sA = (long long)M * K; d.sB = (long long)K * N; d.sC = (long long)M * N;
   d.variant = variant & 15;
   d.prec = variant >> 4;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
-  const size_t ws_n = gemm_workspace_elems(d);
+  unsigned short* planes = nullptr;
+  const int np = d.prec == GEMM_F32 ? 0 : (d.prec == GEMM_BF16 ? 1 : 3);
   hipError_t e = hipMalloc(&A, na * 4);
   if (e == hipSuccess) e = hipMalloc(&Bm, nb * 4);
   if (e == hipSuccess) e = hipMalloc(&Cm, nc * 4);
-  if (e == hipSuccess && ws_n) e = hipMalloc(&ws, ws_n * 4);
   if (e == hipSuccess) e = launch_normal(A, na, 1, 0, st);
   if (e == hipSuccess) e = launch_normal(Bm, nb, 2, 0, st);
   d.A = A; d.B = Bm; d.C = Cm;
+  if (e == hipSuccess && np) {
+    e = hipMalloc(&planes, (size_t)np * (na + nb) * 2);
+    Planes A_{planes, (long long)na, np}, B_{planes + np * na, (long long)nb, np};
+    if (e == hipSuccess) e = launch_split_planes(A, na, A_, st);
+    if (e == hipSuccess) e = launch_split_planes(Bm, nb, B_, st);
+    d.Ap = A_.p; d.pA = A_.stride; d.nA = np;
+    d.Bp = B_.p; d.pB = B_.stride; d.nB = np;
+  }
+  const size_t ws_n = gemm_workspace_elems(d);
+  if (e == hipSuccess && ws_n) e = hipMalloc(&ws, ws_n * 4);
   hipEvent_t t0 = nullptr, t1 = nullptr;
   if (e == hipSuccess) e = hipEventCreate(&t0);
   if (e == hipSuccess) e = hipEventCreate(&t1);
@@ -812,6 +911,20 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   if (t0) (void)hipEventDestroy(t0);
   if (t1) (void)hipEventDestroy(t1);
   for (float* p : {A, Bm, Cm, ws}) if (p) (void)hipFree(p);
+  if (planes) (void)hipFree(planes);
+  if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
+  return MVAE_OK;
+}
+
+extern "C" int mvae_make_batch(const unsigned char* locks, const unsigned char* keys, int height,
+                               int width, const int* idx, const float* coef, int batch,
+                               float* x_out, void* stream) {
+  if (!locks || !keys || !idx || !coef || !x_out || height <= 0 || width <= 0 || batch <= 0)
+    return fail(nullptr, MVAE_EINVAL, "mvae_make_batch: bad argument");
+  if ((reinterpret_cast<uintptr_t>(coef) & 15) != 0)
+    return fail(nullptr, MVAE_EINVAL, "mvae_make_batch: coef must be 16-byte aligned");
+  hipError_t e = launch_make_batch(locks, keys, height, width, idx, coef, batch, 255.f, x_out,
+                                   (hipStream_t)stream);
   if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
   return MVAE_OK;
 }

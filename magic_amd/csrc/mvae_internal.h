@@ -34,6 +34,11 @@ struct GemmEpi {
   float* y = nullptr;           // BCE: optional sigmoid output
   int ldy = 0;
   float* rowpart = nullptr;     // BCE: [M][nblk_n] per-row partial sums of the BCE terms
+  // bf16 planes of the output (same layout/ld as C, plane stride pc): the operand image
+  // of the next GEMM in the bf16 / f32x modes. ncp = 0 (none), 1 (RN) or 3 (exact split).
+  unsigned short* cp = nullptr;
+  long long pc = 0;
+  int ncp = 0;
 };
 
 // bf16 operand shadows (precision = bf16). When set, the GEMM reads A/B from these
@@ -44,9 +49,10 @@ struct GemmDesc {
   const float* B = nullptr; int ldb = 0; bool bt = false;  // bt: B stored [N][K]
   float* C = nullptr; int ldc = 0;
   int batch = 1; long long sA = 0, sB = 0, sC = 0;          // per-batch element strides
-  const __hip_bfloat16* Ah = nullptr;  // bf16 shadows (nullptr = fp32 operands)
-  const __hip_bfloat16* Bh = nullptr;
-  __hip_bfloat16* Ch = nullptr;        // optional bf16 copy of the epilogue output (ldc)
+  // bf16 planes of A and B (bf16 / f32x modes): planes at Ap + i*pA, same layout and ld
+  const unsigned short* Ap = nullptr; long long pA = 0; int nA = 1;
+  const unsigned short* Bp = nullptr; long long pB = 0; int nB = 1;
+  const int* dynA = nullptr;           // != 0 when A's residual planes may be nonzero
   int prec = GEMM_F32;                 // GemmPrec
   int variant = 0;                     // kernel variant (diagnostics / A-B); 0 = default
   int split = 0;                       // forced split-K (0 = planner)
@@ -60,15 +66,21 @@ size_t gemm_workspace_elems(const GemmDesc& d);
 // Launch. ws: device workspace of >= gemm_workspace_elems(d) floats.
 hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t st);
 namespace gemm { struct Params; }
-hipError_t gemm_bf16_launch(const gemm::Params& p, bool at, bool bt, int mode, int epi, hipStream_t st);
+hipError_t gemm_bf16_launch(const gemm::Params& p, const GemmDesc& d, int epi, hipStream_t st);
 // Number of column blocks the BCE epilogue writes per row (rowpart's inner dim).
 int gemm_bce_nblk(int N);
 
 // ---- elementwise / reduction kernels (mvae_kernels.hip) ----
-hipError_t launch_deinterleave(const float* x, float* xs, __hip_bfloat16* xsh, int B, int D, int ldx,
-                               hipStream_t st);
+// bf16 plane image of an fp32 buffer (same layout): planes at p + t*stride, t < n
+struct Planes {
+  unsigned short* p = nullptr;
+  long long stride = 0;
+  int n = 0;
+};
+hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int B, int D,
+                               int ldx, hipStream_t st);
 hipError_t launch_normal(float* out, size_t n, uint64_t seed, uint64_t counter, hipStream_t st);
-hipError_t launch_latent_fwd(const float* ms, const float* eps, float* z, __hip_bfloat16* zh, int B,
+hipError_t launch_latent_fwd(const float* ms, const float* eps, float* z, const Planes& zp, int B,
                              int L, int ldz, hipStream_t st);
 // out[j] for j in [0, ncols): mode 0 = colsq (z_lock^2 | z_key^2), mode 1 = coldot.
 hipError_t launch_colstats(int mode, const float* z, int B, int L, int ldz, const float* colsq,
@@ -82,14 +94,17 @@ hipError_t launch_loss_reduce(const float* rowvals, int B, float inv_bg, float* 
 hipError_t launch_latent_bwd(const float* z, int ldz, const float* ms, const float* eps,
                              const float* dzdec, const float* draw, const float* colsq,
                              const float* coldot, int B, int L, int metric, float w, float inv_bg,
-                             float* dhead, __hip_bfloat16* dheadh, hipStream_t st);
+                             float* dhead, int ldh, const Planes& hp, hipStream_t st);
 struct AdamArgs {
   float* theta; const float* g1; const float* g2; float* m1; float* v1; float* m2; float* v2;
   size_t n_all, n_enc; float lr1, lr2, b1, b2, eps;
-  __hip_bfloat16* theta_h;  // optional bf16 shadow refreshed in the same pass
+  Planes tp;  // bf16 plane image of theta refreshed in the same pass (bf16 / f32x modes)
 };
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
-hipError_t launch_cast_bf16(const float* src, __hip_bfloat16* dst, size_t n, hipStream_t st);
+hipError_t launch_split_planes(const float* src, size_t n, const Planes& dst, hipStream_t st);
+hipError_t launch_make_batch(const unsigned char* locks, const unsigned char* keys, int H, int W,
+                             const int* idx, const float* coef, int B, float div, float* x,
+                             hipStream_t st);
 hipError_t launch_copy2d(const float* src, int lds, float* dst, int ldd, int rows, int cols,
                          hipStream_t st);
 

@@ -13,6 +13,21 @@ namespace {
 
 constexpr float L2_EPS = 1e-12f;  // tf.nn.l2_normalize default
 
+// bf16 plane images of fp32 values (operands of the bf16 / f32x GEMMs): n = 1 round to
+// nearest; n = 3 exact split x = x0 + x1 + x2 (each residual an exact fp32 difference).
+// Returns whether the first residual is nonzero (x not exactly representable in bf16).
+__device__ __forceinline__ bool planes_put(unsigned short* p, long long ps, int n, size_t idx, float v) {
+  float r = v;
+  bool nz = false;
+  for (int t = 0; t < n; ++t) {
+    const unsigned short b = __builtin_bit_cast(unsigned short, __float2bfloat16(r));
+    p[t * ps + idx] = b;
+    r -= __uint_as_float((unsigned)b << 16);
+    if (t == 0) nz = r != 0.f;
+  }
+  return nz;
+}
+
 // internal block (0 rot, 1 lock, 2 key) -> reference eps slot (0 lock, 1 rot, 2 key)
 __device__ __forceinline__ int eps_slot(int blk) { return blk == 0 ? 1 : (blk == 1 ? 0 : 2); }
 
@@ -21,7 +36,8 @@ __device__ __forceinline__ int eps_slot(int blk) { return blk == 0 ? 1 : (blk ==
 //  -> xs[(blk*B + b)][p], blk = {rot:0, lock:1, key:2}. Each thread moves 4 pixels:
 // three 16-B loads, three 16-B stores (coalesced both ways).
 __global__ void deinterleave_vec_kernel(const float4* __restrict__ x, float* __restrict__ xs,
-                                        __hip_bfloat16* __restrict__ xsh, int B, int D, int ldx) {
+                                        unsigned short* __restrict__ xp, long long ps, int np,
+                                        int* __restrict__ dyn, int B, int D, int ldx) {
   const int b = blockIdx.y;
   const int q = blockIdx.x * blockDim.x + threadIdx.x;  // pixel quad
   if (q * 4 >= D) return;
@@ -35,29 +51,37 @@ __global__ void deinterleave_vec_kernel(const float4* __restrict__ x, float* __r
   *reinterpret_cast<float4*>(xs + (size_t)b * ldx + col) = rot;
   *reinterpret_cast<float4*>(xs + (size_t)(B + b) * ldx + col) = lock;
   *reinterpret_cast<float4*>(xs + (size_t)(2 * B + b) * ldx + col) = key;
-  if (xsh) {
+  if (xp) {
     const float4 vv[3] = {rot, lock, key};
+    bool nz = false;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      __hip_bfloat16* d = xsh + (size_t)(c * B + b) * ldx + col;
-      d[0] = __float2bfloat16(vv[c].x); d[1] = __float2bfloat16(vv[c].y);
-      d[2] = __float2bfloat16(vv[c].z); d[3] = __float2bfloat16(vv[c].w);
+      const size_t o = (size_t)(c * B + b) * ldx + col;
+      nz |= planes_put(xp, ps, np, o + 0, vv[c].x);
+      nz |= planes_put(xp, ps, np, o + 1, vv[c].y);
+      nz |= planes_put(xp, ps, np, o + 2, vv[c].z);
+      nz |= planes_put(xp, ps, np, o + 3, vv[c].w);
     }
+    if (dyn && __ballot(nz) != 0 && (threadIdx.x & 63) == 0) atomicOr(dyn, 1);
   }
 }
 
 __global__ void deinterleave_scalar_kernel(const float* __restrict__ x, float* __restrict__ xs,
-                                           __hip_bfloat16* __restrict__ xsh, int B, int D, int ldx) {
+                                           unsigned short* __restrict__ xp, long long ps, int np,
+                                           int* __restrict__ dyn, int B, int D, int ldx) {
   const int b = blockIdx.y;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p >= D) return;
-  const float* src = x + (size_t)b * 3 * D + 3 * (size_t)p;
-  const float v[3] = {src[1], src[0], src[2]};  // rot, lock, key
+  bool nz = false;
+  if (p < D) {
+    const float* src = x + (size_t)b * 3 * D + 3 * (size_t)p;
+    const float v[3] = {src[1], src[0], src[2]};  // rot, lock, key
 #pragma unroll
-  for (int c = 0; c < 3; ++c) {
-    xs[(size_t)(c * B + b) * ldx + p] = v[c];
-    if (xsh) xsh[(size_t)(c * B + b) * ldx + p] = __float2bfloat16(v[c]);
+    for (int c = 0; c < 3; ++c) {
+      xs[(size_t)(c * B + b) * ldx + p] = v[c];
+      if (xp) nz |= planes_put(xp, ps, np, (size_t)(c * B + b) * ldx + p, v[c]);
+    }
   }
+  if (dyn && __ballot(nz) != 0 && (threadIdx.x & 63) == 0) atomicOr(dyn, 1);
 }
 
 // ---------------------------------------------------------------- N(0,1) sampler
@@ -101,8 +125,8 @@ __global__ void normal_kernel(float* __restrict__ out, size_t n, uint64_t seed, 
 // ---------------------------------------------------------------- reparameterisation
 // z = mu + sqrt(exp(s)) * eps   (11a/vae.py:371-377); ms rows = [mu | s] (2L wide)
 __global__ void latent_fwd_kernel(const float* __restrict__ ms, const float* __restrict__ eps,
-                                  float* __restrict__ z, __hip_bfloat16* __restrict__ zh, int B,
-                                  int L, int ldz) {
+                                  float* __restrict__ z, unsigned short* __restrict__ zp,
+                                  long long ps, int np, int B, int L, int ldz) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (size_t)3 * B * L) return;
   const int r = (int)(idx / L), i = (int)(idx - (size_t)r * L);
@@ -112,7 +136,7 @@ __global__ void latent_fwd_kernel(const float* __restrict__ ms, const float* __r
   const float e = eps[((size_t)eps_slot(blk) * B + b) * L + i];
   const float v = mu + sqrtf(expf(s)) * e;
   z[(size_t)r * ldz + i] = v;
-  if (zh) zh[(size_t)r * ldz + i] = __float2bfloat16(v);
+  if (zp) planes_put(zp, ps, np, (size_t)r * ldz + i, v);
 }
 
 // ---------------------------------------------------------------- column statistics
@@ -258,8 +282,8 @@ __global__ void latent_bwd_kernel(const float* __restrict__ z, int ldz, const fl
                                   const float* __restrict__ eps, const float* __restrict__ dzdec,
                                   const float* __restrict__ draw, const float* __restrict__ colsq,
                                   const float* __restrict__ coldot, int B, int L, int metric,
-                                  float w, float inv_bg, float* __restrict__ dhead,
-                                  __hip_bfloat16* __restrict__ dheadh) {
+                                  float w, float inv_bg, float* __restrict__ dhead, int ldh,
+                                  unsigned short* __restrict__ hp, long long ps, int np) {
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= (size_t)4 * B * L) return;
   const int r = (int)(idx / L), i = (int)(idx - (size_t)r * L);
@@ -295,11 +319,11 @@ __global__ void latent_bwd_kernel(const float* __restrict__ z, int ldz, const fl
   }
   const float dmu = dz + dmu_extra;
   const float ds = 0.5f * dz * e * sig + ds_extra;
-  dhead[(size_t)r * 2 * L + i] = dmu;
-  dhead[(size_t)r * 2 * L + L + i] = ds;
-  if (dheadh) {
-    dheadh[(size_t)r * 2 * L + i] = __float2bfloat16(dmu);
-    dheadh[(size_t)r * 2 * L + L + i] = __float2bfloat16(ds);
+  dhead[(size_t)r * ldh + i] = dmu;
+  dhead[(size_t)r * ldh + L + i] = ds;
+  if (hp) {
+    planes_put(hp, ps, np, (size_t)r * ldh + i, dmu);
+    planes_put(hp, ps, np, (size_t)r * ldh + L + i, ds);
   }
 }
 
@@ -328,12 +352,13 @@ __global__ void adam_kernel(AdamArgs a) {
     th -= (a.lr2 * m) / (sqrtf(v) + a.eps);
   }
   a.theta[i] = th;
-  if (a.theta_h) a.theta_h[i] = __float2bfloat16(th);
+  if (a.tp.p) planes_put(a.tp.p, a.tp.stride, a.tp.n, i, th);
 }
 
-__global__ void cast_bf16_kernel(const float* __restrict__ s, __hip_bfloat16* __restrict__ d, size_t n) {
+__global__ void split_planes_kernel(const float* __restrict__ s, size_t n, unsigned short* p,
+                                    long long ps, int np) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) d[i] = __float2bfloat16(s[i]);
+  if (i < n) planes_put(p, ps, np, i, s[i]);
 }
 
 __global__ void copy2d_kernel(const float* __restrict__ s, int lds, float* __restrict__ d, int ldd,
@@ -344,19 +369,52 @@ __global__ void copy2d_kernel(const float* __restrict__ s, int lds, float* __res
   d[(size_t)r * ldd + c] = s[(size_t)r * lds + c];
 }
 
+// ---------------------------------------------------------------- batch producer
+// The reference's input pipeline for one batch (11a/overlap_input.py:127-261): lock and key
+// images from uint8 tables, the lock rotated by tf.contrib.image.rotate semantics (output
+// (x,y) samples ((c*x - s*y) + x_off, (s*x + c*y) + y_off), NEAREST = roundf, zero fill;
+// per-example coefficients precomputed in fp32 on the host), concatenated per pixel as
+// (lock, rotated, key) and divided by 255 -> X [B, H*W*3]. No FMA contraction, so the
+// gather indices match the host restatement bit for bit.
+__global__ void make_batch_kernel(const unsigned char* __restrict__ locks,
+                                  const unsigned char* __restrict__ keys, int H, int W,
+                                  const int* __restrict__ idx, const float4* __restrict__ coef,
+                                  float div, float* __restrict__ x) {
+  const int b = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  const int HW = H * W;
+  if (p >= HW) return;
+  const int id = idx[b];
+  const float4 cf = coef[b];
+  const int yy = p / W, xx = p - yy * W;
+  const float fx = (float)xx, fy = (float)yy;
+  const float xin = __fadd_rn(__fsub_rn(__fmul_rn(cf.x, fx), __fmul_rn(cf.y, fy)), cf.z);
+  const float yin = __fadd_rn(__fadd_rn(__fmul_rn(cf.y, fx), __fmul_rn(cf.x, fy)), cf.w);
+  const float xr = roundf(xin), yr = roundf(yin);
+  const unsigned char* L = locks + (size_t)id * HW;
+  float rot = 0.f;
+  if (xr >= 0.f && xr <= (float)(W - 1) && yr >= 0.f && yr <= (float)(H - 1))
+    rot = (float)L[(int)yr * W + (int)xr];
+  float* o = x + (size_t)b * 3 * HW + 3 * (size_t)p;
+  o[0] = (float)L[p] / div;
+  o[1] = rot / div;
+  o[2] = (float)keys[(size_t)id * HW + p] / div;
+}
+
 inline unsigned nblocks(size_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 }  // namespace
 
-hipError_t launch_deinterleave(const float* x, float* xs, __hip_bfloat16* xsh, int B, int D,
+hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int B, int D,
                                int ldx, hipStream_t st) {
   if ((D % 4) == 0 && (reinterpret_cast<uintptr_t>(x) % 16) == 0 && (ldx % 4) == 0) {
     dim3 g(nblocks(D / 4, 256), B);
     hipLaunchKernelGGL(deinterleave_vec_kernel, g, dim3(256), 0, st,
-                       reinterpret_cast<const float4*>(x), xs, xsh, B, D, ldx);
+                       reinterpret_cast<const float4*>(x), xs, xp.p, xp.stride, xp.n, dyn, B, D, ldx);
   } else {
     dim3 g(nblocks(D, 256), B);
-    hipLaunchKernelGGL(deinterleave_scalar_kernel, g, dim3(256), 0, st, x, xs, xsh, B, D, ldx);
+    hipLaunchKernelGGL(deinterleave_scalar_kernel, g, dim3(256), 0, st, x, xs, xp.p, xp.stride, xp.n,
+                       dyn, B, D, ldx);
   }
   return hipGetLastError();
 }
@@ -366,10 +424,11 @@ hipError_t launch_normal(float* out, size_t n, uint64_t seed, uint64_t counter, 
   return hipGetLastError();
 }
 
-hipError_t launch_latent_fwd(const float* ms, const float* eps, float* z, __hip_bfloat16* zh, int B,
+hipError_t launch_latent_fwd(const float* ms, const float* eps, float* z, const Planes& zp, int B,
                              int L, int ldz, hipStream_t st) {
   const size_t n = (size_t)3 * B * L;
-  hipLaunchKernelGGL(latent_fwd_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, ms, eps, z, zh, B, L, ldz);
+  hipLaunchKernelGGL(latent_fwd_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, ms, eps, z, zp.p,
+                     zp.stride, zp.n, B, L, ldz);
   return hipGetLastError();
 }
 
@@ -401,10 +460,10 @@ hipError_t launch_loss_reduce(const float* rowvals, int B, float inv_bg, float* 
 hipError_t launch_latent_bwd(const float* z, int ldz, const float* ms, const float* eps,
                              const float* dzdec, const float* draw, const float* colsq,
                              const float* coldot, int B, int L, int metric, float w, float inv_bg,
-                             float* dhead, __hip_bfloat16* dheadh, hipStream_t st) {
+                             float* dhead, int ldh, const Planes& hp, hipStream_t st) {
   const size_t n = (size_t)4 * B * L;
   hipLaunchKernelGGL(latent_bwd_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, z, ldz, ms, eps, dzdec,
-                     draw, colsq, coldot, B, L, metric, w, inv_bg, dhead, dheadh);
+                     draw, colsq, coldot, B, L, metric, w, inv_bg, dhead, ldh, hp.p, hp.stride, hp.n);
   return hipGetLastError();
 }
 
@@ -413,8 +472,19 @@ hipError_t launch_adam(const AdamArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_cast_bf16(const float* src, __hip_bfloat16* dst, size_t n, hipStream_t st) {
-  hipLaunchKernelGGL(cast_bf16_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, src, dst, n);
+hipError_t launch_split_planes(const float* src, size_t n, const Planes& dst, hipStream_t st) {
+  if (!dst.p || n == 0) return hipSuccess;
+  hipLaunchKernelGGL(split_planes_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, src, n, dst.p,
+                     dst.stride, dst.n);
+  return hipGetLastError();
+}
+
+hipError_t launch_make_batch(const unsigned char* locks, const unsigned char* keys, int H, int W,
+                             const int* idx, const float* coef, int B, float div, float* x,
+                             hipStream_t st) {
+  dim3 g(nblocks((size_t)H * W, 256), B);
+  hipLaunchKernelGGL(make_batch_kernel, g, dim3(256), 0, st, locks, keys, H, W, idx,
+                     reinterpret_cast<const float4*>(coef), div, x);
   return hipGetLastError();
 }
 

@@ -123,10 +123,16 @@ class Engine:
     def params(self) -> Dict[str, torch.Tensor]:
         return self.tensors(_lib.KIND_PARAM)
 
+    def sync_params(self):
+        """Refresh the bf16 plane images of the parameters after writing the fp32 masters
+        through the views (bf16 / f32x modes; a no-op in fp32 mode)."""
+        self._check(self.lib.mvae_sync_params(self.ctx, self.stream))
+
     def load_params(self, P: Dict[str, np.ndarray]):
         views = self.params()
         for k, v in P.items():
             views[k].copy_(torch.as_tensor(np.asarray(v, np.float32)).to(self.dev))
+        self.sync_params()
         torch.cuda.synchronize(self.dev)
 
     def init_params(self, seed: int = 0):
@@ -141,6 +147,7 @@ class Engine:
                 v.copy_(torch.from_numpy(rng.uniform(-hi, hi, size=(fan_in, fan_out)).astype(np.float32)).to(self.dev))
             else:
                 v.zero_()
+        self.sync_params()
         torch.cuda.synchronize(self.dev)
 
     def get_step(self):

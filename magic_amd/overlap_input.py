@@ -1,4 +1,5 @@
-"""Batch producer with the reference's layout (``11a/overlap_input.py:76-261``).
+"""Batch producer with the reference's layout (``11a/overlap_input.py:76-261``), assembled on
+the GPU by the HIP kernel ``mvae_make_batch``.
 
 ``inputs(normalize=True, reshape=True, rotation=True)`` returns a ``BatchStream``; each
 ``next(stream)`` (the reference's ``sess.run([images_batch, labels_batch])``) yields
@@ -12,8 +13,8 @@ Sources: a directory or .zip of ``{N}_L.png`` / ``{N}_K.png`` pairs with an area
 (``.npy``), or the synthetic shape generator (``synthetic=True``; BASELINE.json asks for
 100x100 synthetic pairs). The rotated lock is the lock rotated by U[0, 2pi) about the image
 centre with nearest-neighbour sampling and zero fill, the ``tf.contrib.image.rotate``
-semantics (``11a/utils.py:453-464``). Rotation and assembly run as torch ops on the
-stream's device (input plumbing, outside the timed training step).
+semantics (``11a/utils.py:453-464``); decoded images live in HBM as uint8 tables and each
+batch is gathered, rotated, interleaved and normalised by one HIP kernel.
 """
 from __future__ import annotations
 
@@ -29,34 +30,34 @@ import torch
 from .constants import FLAGS
 
 
-def rotate_nearest(img: torch.Tensor, angle: torch.Tensor) -> torch.Tensor:
-    """``tf.contrib.image.rotate(images, angles)`` (NEAREST, zero fill) for img [N, H, W].
-
-    Output pixel (x, y) samples input (x', y') = R(angle)·(x, y) + offset with
-    R = [[cos, -sin], [sin, cos]], offset so the centre ((W-1)/2, (H-1)/2) is fixed;
-    nearest = round half away from zero."""
-    n, h, w = img.shape
-    dev = img.device
-    a = angle.to(dev, torch.float32).reshape(n, 1, 1)
-    c, s = torch.cos(a), torch.sin(a)
-    xo = ((w - 1) - (c * (w - 1) - s * (h - 1))) / 2.0
-    yo = ((h - 1) - (s * (w - 1) + c * (h - 1))) / 2.0
-    ys, xs = torch.meshgrid(torch.arange(h, device=dev, dtype=torch.float32),
-                            torch.arange(w, device=dev, dtype=torch.float32), indexing="ij")
-    xin = c * xs - s * ys + xo
-    yin = s * xs + c * ys + yo
-    xr = torch.sign(xin) * torch.floor(torch.abs(xin) + 0.5)
-    yr = torch.sign(yin) * torch.floor(torch.abs(yin) + 0.5)
-    inside = (xr >= 0) & (xr <= w - 1) & (yr >= 0) & (yr <= h - 1)
-    idx = (yr.clamp(0, h - 1) * w + xr.clamp(0, w - 1)).long()
-    out = torch.gather(img.reshape(n, h * w), 1, idx.reshape(n, h * w)).reshape(n, h, w)
-    return torch.where(inside, out, torch.zeros((), device=dev, dtype=img.dtype))
+def rotation_coefficients(angles, height: int, width: int) -> np.ndarray:
+    """Per-example ``tf.contrib.image.rotate`` coefficients (cos, sin, x_off, y_off), float32
+    as TF's ``angles_to_projective_transforms`` computes them; [B] radians -> [B, 4]."""
+    a = np.asarray(angles, np.float32)
+    c = np.cos(a).astype(np.float32)
+    s = np.sin(a).astype(np.float32)
+    w1, h1 = np.float32(width - 1), np.float32(height - 1)
+    xo = ((w1 - (c * w1 - s * h1)) / np.float32(2.0)).astype(np.float32)
+    yo = ((h1 - (s * w1 + c * h1)) / np.float32(2.0)).astype(np.float32)
+    return np.ascontiguousarray(np.stack([c, s, xo, yo], axis=1), dtype=np.float32)
 
 
-def assemble(lock: torch.Tensor, rot: torch.Tensor, key: torch.Tensor) -> torch.Tensor:
-    """[N,H,W] x3 -> [N, H*W*3] channel-interleaved (lock, rotated lock, key)."""
-    n = lock.shape[0]
-    return torch.stack([lock, rot, key], dim=3).reshape(n, -1).contiguous()
+def make_batch(locks: torch.Tensor, keys: torch.Tensor, idx: torch.Tensor, coef: torch.Tensor,
+               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """HIP batch producer (``mvae_make_batch``): uint8 device tables [n, H, W], idx int32 [B],
+    coef float32 [B, 4] -> X float32 [B, H*W*3] = per pixel (lock, rotated lock, key) / 255."""
+    from . import _lib
+    lib = _lib.load()
+    n, h, w = locks.shape
+    B = idx.shape[0]
+    for t, dt in ((locks, torch.uint8), (keys, torch.uint8), (idx, torch.int32), (coef, torch.float32)):
+        if not t.is_cuda or t.dtype != dt or not t.is_contiguous():
+            raise ValueError("make_batch: device tensors (uint8 tables, int32 idx, float32 coef) expected")
+    out = out if out is not None else torch.empty(B, 3 * h * w, device=locks.device)
+    rc = lib.mvae_make_batch(locks.data_ptr(), keys.data_ptr(), h, w, idx.data_ptr(), coef.data_ptr(),
+                             B, out.data_ptr(), torch.cuda.current_stream(locks.device).cuda_stream)
+    _lib.check(lib, None, rc)
+    return out
 
 
 def random_shapes(n: int, size: int, gen: torch.Generator, device) -> torch.Tensor:
@@ -102,16 +103,18 @@ def area_distribution() -> np.ndarray:
 
 def synthetic_batch(batch: int, image_size: int, seed: int = 1, device="cuda",
                     dtype=torch.float32) -> Tuple[torch.Tensor, torch.Tensor]:
-    """One seeded synthetic batch (X [B, 3D] in {0,1}, areas [B])."""
+    """One seeded synthetic batch (X [B, 3D] in {0,1}, areas [B]) through the HIP producer."""
     gen = torch.Generator().manual_seed(seed)
-    lock = random_shapes(batch, image_size, gen, device)
-    key = random_shapes(batch, image_size, gen, device)
-    ang = torch.rand(batch, generator=gen) * (2 * math.pi)
-    rot = rotate_nearest(lock, ang)
-    x = assemble(lock, rot, key).to(dtype)
+    dev = torch.device(device)
+    lock = (random_shapes(batch, image_size, gen, device) * 255).to(torch.uint8).contiguous()
+    key = (random_shapes(batch, image_size, gen, device) * 255).to(torch.uint8).contiguous()
+    ang = torch.rand(batch, generator=gen).numpy() * (2 * math.pi)
+    coef = torch.from_numpy(rotation_coefficients(ang, image_size, image_size)).to(dev)
+    idx = torch.arange(batch, dtype=torch.int32, device=dev)
+    x = make_batch(lock, key, idx, coef).to(dtype)
     dist = area_distribution()
-    idx = torch.randint(0, len(dist), (batch,), generator=gen).numpy()
-    areas = torch.from_numpy(dist[idx]).to(device)
+    sel = torch.randint(0, len(dist), (batch,), generator=gen).numpy()
+    areas = torch.from_numpy(dist[sel]).to(dev)
     return x, areas
 
 
@@ -145,62 +148,75 @@ class PairSource:
             areas = area_distribution()
         self.areas = np.asarray(areas, np.float32)[:i]
 
+    @classmethod
+    def from_packed(cls, npz_path: str, areas: Optional[np.ndarray] = None, limit: Optional[int] = None):
+        """Pairs from a packed-bit archive (``lock_bits``, ``key_bits``, ``shape``) such as
+        tests/golden/overlap_micro.npz, the reference's overlap_micro.zip images."""
+        z = np.load(npz_path)
+        n, h, w = (int(v) for v in z["shape"])
+        n = n if limit is None else min(n, limit)
+        self = cls.__new__(cls)
+        self.locks = np.unpackbits(z["lock_bits"][:n], axis=-1)[..., :w].astype(np.float32) * 255.0
+        self.keys = np.unpackbits(z["key_bits"][:n], axis=-1)[..., :w].astype(np.float32) * 255.0
+        self.areas = np.asarray(areas if areas is not None else area_distribution(), np.float32)[:n]
+        return self
+
     def __len__(self):
         return len(self.locks)
 
 
 class BatchStream:
     """Shuffled epochs over a source (``slice_input_producer(shuffle=True)`` +
-    ``shuffle_batch``), random rotation per example, /255 normalisation."""
+    ``shuffle_batch``), a uniform [0, 2pi) rotation per example, /255 normalisation — the
+    per-batch assembly runs in the HIP batch producer (``mvae_make_batch``)."""
 
     def __init__(self, batch: int, image_size: int, source: Optional[PairSource] = None,
                  normalize: bool = True, seed: int = 1, device="cuda", synthetic_pool: int = 960):
-        self.batch, self.size, self.normalize = batch, image_size, normalize
+        if not normalize:
+            raise ValueError("the HIP batch producer emits normalised pixels (/255)")
+        self.batch, self.size = batch, image_size
         self.device = torch.device(device)
-        self.gen = torch.Generator().manual_seed(seed)
+        self.rng = np.random.default_rng(seed)
         if source is None:  # synthetic pool of pairs, re-rotated every draw
             g = torch.Generator().manual_seed(seed + 1000)
             lock = random_shapes(synthetic_pool, image_size, g, "cpu") * 255.0
             key = random_shapes(synthetic_pool, image_size, g, "cpu") * 255.0
             dist = area_distribution()
             idx = torch.randint(0, len(dist), (synthetic_pool,), generator=g).numpy()
-            self.locks, self.keys, self.areas = lock, key, torch.from_numpy(dist[idx])
+            locks, keys, self.areas = lock, key, torch.from_numpy(dist[idx])
         else:
             if source.locks.shape[1] != image_size:
                 raise ValueError(f"images are {source.locks.shape[1]}px, expected {image_size}")
-            self.locks = torch.from_numpy(source.locks)
-            self.keys = torch.from_numpy(source.keys)
+            locks, keys = torch.from_numpy(source.locks), torch.from_numpy(source.keys)
             self.areas = torch.from_numpy(source.areas)
-        self.locks = self.locks.to(self.device)
-        self.keys = self.keys.to(self.device)
-        self._perm = torch.empty(0, dtype=torch.long)
+        self.locks = locks.round().clamp(0, 255).to(torch.uint8).contiguous().to(self.device)
+        self.keys = keys.round().clamp(0, 255).to(torch.uint8).contiguous().to(self.device)
+        self.areas = self.areas.float().to(self.device)
+        self._perm = np.empty(0, dtype=np.int64)
         self._pos = 0
 
     def _take(self, n):
         out = []
         while n > 0:
             if self._pos >= len(self._perm):
-                self._perm = torch.randperm(len(self.locks), generator=self.gen)
+                self._perm = self.rng.permutation(len(self.locks))
                 self._pos = 0
             k = min(n, len(self._perm) - self._pos)
             out.append(self._perm[self._pos:self._pos + k])
             self._pos += k
             n -= k
-        return torch.cat(out)
+        return np.concatenate(out)
 
     def __iter__(self) -> Iterator:
         return self
 
     def __next__(self):
         idx = self._take(self.batch)
-        lock = self.locks[idx.to(self.device)]
-        key = self.keys[idx.to(self.device)]
-        ang = torch.rand(self.batch, generator=self.gen) * (2 * math.pi)
-        rot = rotate_nearest(lock, ang)
-        x = assemble(lock, rot, key)
-        if self.normalize:
-            x = x / 255.0
-        return x.contiguous(), self.areas[idx].to(self.device).float()
+        ang = self.rng.uniform(0.0, 2 * math.pi, self.batch)
+        coef = torch.from_numpy(rotation_coefficients(ang, self.size, self.size)).to(self.device)
+        idx_t = torch.from_numpy(idx.astype(np.int32)).to(self.device)
+        x = make_batch(self.locks, self.keys, idx_t, coef)
+        return x, self.areas[idx_t.long()]
 
 
 def inputs(normalize: bool = False, reshape: bool = False, rotation: bool = False,
@@ -212,5 +228,8 @@ def inputs(normalize: bool = False, reshape: bool = False, rotation: bool = Fals
     size = image_size or FLAGS.IMAGE_SIZE
     bs = batch_size or FLAGS.BATCH_SIZE
     d = data_dir if data_dir is not None else FLAGS.DATA_DIR
-    src = PairSource(d, limit=FLAGS.NUM_EXAMPLES_TO_LOAD_INTO_QUEUE) if d else None
+    src = None
+    if d:
+        lim = FLAGS.NUM_EXAMPLES_TO_LOAD_INTO_QUEUE
+        src = PairSource.from_packed(d, limit=lim) if d.endswith(".npz") else PairSource(d, limit=lim)
     return BatchStream(bs, size, src, normalize=normalize, seed=seed, device=device)

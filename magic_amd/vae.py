@@ -131,6 +131,7 @@ class TangoEncoder(object):
                 v.copy_(sd[f"{tag}/{k}"].to(v.device))
         t1, t2 = (int(x) for x in sd["step"])
         self.engine.set_step(t1, t2)
+        self.engine.sync_params()
         torch.cuda.synchronize(self.engine.dev)
 
     def close(self):

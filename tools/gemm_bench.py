@@ -37,7 +37,7 @@ def shapes(cfg):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,16,32")
+    ap.add_argument("--variants", default="0,16,17,18,32")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--config", default="C2")
