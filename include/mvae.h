@@ -121,6 +121,12 @@ int mvae_forward(mvae_ctx* ctx, const float* x, const float* eps, void* stream);
 int mvae_metric(mvae_ctx* ctx, const float* areas, void* stream);
 /* Needs MVAE_BUF_COLDOT summed over ranks (cosine). Writes MVAE_BUF_GRADS.           */
 int mvae_backward(mvae_ctx* ctx, void* stream);
+/* The same backward in three parts (0: decoder; 1: latent head, encoder dgrad chain and
+ * the layer-0 weight gradient; 2: the remaining encoder weight gradients). After part k,
+ * the ranges mvae_grad_range(ctx, k, i = 0, 1, ...) are final: a data-parallel host
+ * all-reduces them while the later parts run (returns MVAE_EINVAL past the last range). */
+int mvae_backward_part(mvae_ctx* ctx, int part, void* stream);
+int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* count);
 /* Both TF ApplyAdam updates from MVAE_BUF_GRADS (theta -= d1(g1) + d2(g2)).           */
 int mvae_adam(mvae_ctx* ctx, void* stream);
 /* Single-GPU partial_fit: all four phases. losses_out: device float[5] or NULL;
@@ -153,8 +159,9 @@ int mvae_timing_read(mvae_ctx* ctx, int region, double* total_ms, int64_t* count
 int mvae_timing_reset(mvae_ctx* ctx);
 /* One GEMM of the step's kernel family: C[M,N] = epi(A[M,K] B[K,N]); A stored [M][K]
  * (at=0) or [K][M] (at=1), B stored [K][N] (bt=0) or [N][K] (bt=1). epi: 0 store,
- * 1 act (act: 0 tanh, 1 elu), 2 C = acc * act'(aux), 4 sigmoid; epi | (prec << 4)
- * selects the arithmetic (MVAE_PREC_*). Workspace is allocated and freed inside
+ * 1 act (act: 0 tanh, 1 elu), 2 C = acc * act'(aux), 4 sigmoid; epi | (prec << 4) |
+ * (variant << 8) selects the arithmetic (MVAE_PREC_*) and kernel (0 auto, 3 the 256x256
+ * bf16 kernel, 4 the 128x128 one). Workspace is allocated and freed inside
  * (synchronous; tests only). mvae_bench_gemm: variant | (prec << 4).                 */
 int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, int variant, int iters,
                     void* stream, float* avg_ms);

@@ -19,6 +19,9 @@
 //     ds_read_b64_tr_b16 (CDNA4 transposing LDS read), conflict-free.
 #include "gemm_common.h"
 
+#include <cmath>
+#include <cstdint>
+
 namespace mvae {
 namespace {
 
@@ -44,6 +47,7 @@ struct PParams {
   const unsigned short* B; long long pB;
   int npairs, npairs0;
   unsigned char pa[6], pb[6];
+  int pab;                          // pa[i] | pb[i] << 2 packed 4 bits per pair (no memory reads)
   const int* dyn;                   // A residual planes nonzero? (nullptr: use all pairs)
 };
 
@@ -191,6 +195,197 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16p_kernel(PParams pp) {
   epilogue<EPI>(p, t, acc, reinterpret_cast<float*>(smem));
 }
 
+// ---------------------------------------------------------------------------------------
+// Wide kernel: 256x256x64 tile, 512 threads = 8 waves (2 along M x 4 along N), each wave
+// 128x64 = 4x2 MFMA 32x32x16 accumulators (1024 MFMA cycles per k-tile per wave). Operand
+// tiles are copied HBM -> LDS by global_load_lds_dwordx4 (no VGPR staging): two LDS stages
+// of 2 x 32 KB, the next k-tile's copy in flight during the MFMAs of the current one, one
+// barrier per k-tile. The LDS images are lane-linear (the DMA's destination is wave base +
+// 16 B x lane); bank-conflict-free fragment reads come from XOR swizzles applied to the
+// per-lane SOURCE address and undone on the read:
+//   k-contiguous operand: image [256 rows][8 chunks of 8 k], chunk c of row r at position
+//     c ^ ((r >> 1) & 7)  -> ds_read_b128 of 16 consecutive rows hits 16 distinct 16-B slots;
+//   row-contiguous operand: image [64 k][32 chunks of 8 rows], chunk c of k-row k at
+//     position c ^ (4 (k & 3))  -> the 32 lanes of a ds_read_b64_tr_b16 pass hit 32 slots.
+// Out-of-range chunks (k >= ke, rows >= nrows of a row-contiguous operand) are loaded from a
+// zero page, so partial tiles need no masking; rows past the end of a k-contiguous operand
+// are clamped (their outputs are not stored). Requires every ld, batch and plane stride and
+// the K padding [K, round8(K)) of k-contiguous operands to be zero-filled multiples of 8.
+constexpr int WT = 256, WNT = 512, WBK = 64;
+constexpr int WIMG = WT * WBK;  // bf16 elements per operand image
+
+__device__ __attribute__((aligned(16))) int4 g_zero16[1];
+typedef __attribute__((address_space(3))) short lds_short;
+
+template <bool KC>
+struct WLoad {
+  long long off[4];
+  int kc[4];
+  bool rv[4];
+  __device__ __forceinline__ void init(int ld, int r0, int nrows, int wave, int lane) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q0 = j * 8 + wave;  // 64-chunk group of this wave-instruction
+      if constexpr (KC) {
+        const int row = q0 * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        int gr = r0 + row;
+        gr = gr < nrows ? gr : nrows - 1;
+        off[j] = (long long)gr * ld + 8 * c;
+        kc[j] = 8 * c;
+        rv[j] = true;
+      } else {
+        const int krow = q0 * 2 + (lane >> 5);
+        const int c = (lane & 31) ^ (4 * (krow & 3));
+        const int col = r0 + 8 * c;
+        rv[j] = col < nrows;
+        off[j] = (long long)krow * ld + col;
+        kc[j] = krow;
+      }
+    }
+  }
+  __device__ __forceinline__ void issue(const unsigned short* __restrict__ g, int ld, int k0,
+                                        int kend, short* img, int wave) const {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const bool ok = rv[j] && k0 + kc[j] < kend;
+      const unsigned short* src = KC ? g + off[j] + k0 : g + off[j] + (long long)k0 * ld;
+      src = ok ? src : reinterpret_cast<const unsigned short*>(g_zero16);
+      __builtin_amdgcn_global_load_lds(src, (lds_short*)(img + (j * 8 + wave) * 512), 16, 0, 0);
+    }
+  }
+  // LDS instructions per fragment
+  static constexpr int NRD = KC ? 1 : 2;
+  // fragment (8 consecutive k) of the 32-row block at rb, k16-step ks. The transposing reads
+  // are inline asm: the builtin makes hipcc wait for every outstanding LDS-DMA (vmcnt(0))
+  // before it, serialising the next tile's copy with this tile's MFMAs. Their results are
+  // waited for explicitly (wait_frags) before use.
+  __device__ __forceinline__ bf16x8 frag(const short* s, unsigned s_lds, int rb, int ks,
+                                         int lane) const {
+    if constexpr (KC) {
+      const int row = rb + (lane & 31);
+      const int pos = (2 * ks + (lane >> 5)) ^ ((row >> 1) & 7);
+      const s16x8 v = *reinterpret_cast<const s16x8*>(s + row * WBK + pos * 8);
+      return __builtin_bit_cast(bf16x8, v);
+    } else {
+      const int i = lane & 15, q = i >> 2, pp = i & 3;
+      const int kk = 16 * ks + 8 * (lane >> 5) + q;
+      const int ro = rb + 16 * ((lane >> 4) & 1) + 4 * pp;
+      const int pos = (ro >> 3) ^ (4 * (kk & 3));
+      const unsigned a0 = s_lds + 2u * (unsigned)(kk * WT + pos * 8 + (ro & 4));
+      s16x4 lo, hi;
+      asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a0), "i"(8 * WT));
+      return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+    }
+  }
+};
+
+// wait until at most n LDS instructions are outstanding (n is a literal per instantiation)
+template <int N>
+__device__ __forceinline__ void wait_lds() {
+  if constexpr (N == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+  else if constexpr (N == 6) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
+  else if constexpr (N == 8) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+  else if constexpr (N == 10) asm volatile("s_waitcnt lgkmcnt(10)" ::: "memory");
+  else if constexpr (N == 12) asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
+  else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}
+
+template <bool AT, bool BT, int EPI>
+__global__ __launch_bounds__(WNT, 1) void gemm_bf16w_kernel(PParams pp) {
+  const Params& p = pp.g;
+  __shared__ __attribute__((aligned(16))) short smem[4 * WIMG];  // [stage][A | B]
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const Tile t = tile_of_t<WT, WT>(p, true);
+  const unsigned short* __restrict__ A = pp.A + t.bi * p.sA;
+  const unsigned short* __restrict__ Bm = pp.B + t.bi * p.sB;
+
+  WLoad<!AT> la;
+  WLoad<BT> lb;
+  la.init(p.lda, t.m0, p.M, wave, lane);
+  lb.init(p.ldb, t.n0, p.N, wave, lane);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int npairs = (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
+  const int nkt = t.ks < t.ke ? (t.ke - t.ks + WBK - 1) / WBK : 0;
+  const int total = npairs * nkt;
+  int ipr = 0, ikt = 0;  // (pair, k-tile) of the next copy
+  auto issue = [&](int stage) {
+    short* img = smem + stage * 2 * WIMG;
+    const int k0 = t.ks + ikt * WBK;
+    const int pab = pp.pab >> (4 * ipr);
+    la.issue(A + (pab & 3) * pp.pA, p.lda, k0, t.ke, img, wave);
+    lb.issue(Bm + ((pab >> 2) & 3) * pp.pB, p.ldb, k0, t.ke, img + WIMG, wave);
+    if (++ikt == nkt) { ikt = 0; ++ipr; }
+  };
+  constexpr int NRD = 4 * WLoad<!AT>::NRD + 2 * WLoad<BT>::NRD;  // LDS reads per k16-step
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
+  if (total > 0) issue(0);
+  for (int it = 0; it < total; ++it) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage it&1 landed for all waves; stage (it+1)&1 no longer read
+    if (it + 1 < total) issue((it + 1) & 1);
+    const short* sa = smem + (it & 1) * 2 * WIMG;
+    const short* sb = sa + WIMG;
+    const unsigned la0 = lds0 + 2u * (unsigned)((it & 1) * 2 * WIMG);
+    const unsigned lb0 = la0 + 2u * WIMG;
+    bf16x8 fa[2][4], fb[2][2];
+    auto rd = [&](int ks, bf16x8 (&a)[4], bf16x8 (&b)[2]) {
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) b[ni] = lb.frag(sb, lb0, wn * 64 + ni * 32, ks, lane);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) a[mi] = la.frag(sa, la0, wm * 128 + mi * 32, ks, lane);
+    };
+    rd(0, fa[0], fb[0]);
+#pragma unroll
+    for (int ks = 0; ks < WBK / 16; ++ks) {
+      if (ks + 1 < WBK / 16) {
+        rd(ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
+        wait_lds<NRD>();
+      } else {
+        wait_lds<0>();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks & 1][mi], fb[ks & 1][ni],
+                                                                acc[mi][ni], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  __syncthreads();
+  epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
+}
+
+template <bool AT, bool BT, int EPI>
+hipError_t launch_w(const PParams& p, hipStream_t st) {
+  const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
+  hipLaunchKernelGGL((gemm_bf16w_kernel<AT, BT, EPI>), dim3(nwg), dim3(WNT), 0, st, p);
+  return hipGetLastError();
+}
+
+template <int EPI>
+hipError_t launch_wide(const PParams& p, bool at, bool bt, hipStream_t st) {
+  if (!at && !bt) return launch_w<false, false, EPI>(p, st);
+  if (at && !bt) return launch_w<true, false, EPI>(p, st);
+  if (!at && bt) return launch_w<false, true, EPI>(p, st);
+  return launch_w<true, true, EPI>(p, st);
+}
+
 template <bool AT, bool BT, int EPI, int BK, bool DB>
 hipError_t launch_t(const PParams& p, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
@@ -221,6 +416,42 @@ hipError_t launch_var(const PParams& p, bool at, bool bt, int variant, hipStream
 
 }  // namespace
 
+bool gemm_bf16_wide(const GemmDesc& d) {
+  if (d.prec == GEMM_F32) return false;
+  if (d.variant == 1 || d.variant == 2 || d.variant == 4) return false;  // 128x128 variants
+  if (d.variant != 3 && (d.M < 256 || d.N < 256)) return false;
+  auto a8 = [](long long v) { return (v & 7) == 0; };
+  if (!a8(d.lda) || !a8(d.ldb) || !a8(d.pA) || !a8(d.pB)) return false;
+  if (d.batch > 1 && (!a8(d.sA) || !a8(d.sB))) return false;
+  if ((reinterpret_cast<uintptr_t>(d.Ap) | reinterpret_cast<uintptr_t>(d.Bp)) & 15) return false;
+  return true;
+}
+
+int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws) {
+  if (d.epi.mode == EPI_BCE || d.epi.mode == EPI_SIGMOID) return 1;
+  const long long tiles = (long long)((d.M + WT - 1) / WT) * ((d.N + WT - 1) / WT) * d.batch;
+  const int kt = (d.K + WBK - 1) / WBK;
+  const int T = d.nA > d.nB ? d.nA : d.nB;
+  int np = 0;
+  for (int i = 0; i < d.nA; ++i)
+    for (int j = 0; j < d.nB; ++j) np += i + j < T;
+  if (d.dynA) np = (np + (d.nB < T ? d.nB : T)) / 2;  // A's residual planes often all zero
+  // one 256x256x64 k-tile per CU ~1.07 us (MFMA-bound, 2 waves/SIMD); + prologue/epilogue;
+  // split-K adds the fp32 slab round trip and the reduction launch
+  const double t_kt = 1.07e-6;
+  double best = 1e30;
+  int best_s = 1;
+  for (int s = 1; s <= 32; ++s) {
+    if (s > 1 && kt / s < 2) break;
+    if (s > 1 && (size_t)d.batch * s * d.M * d.N > max_ws) break;
+    const double rounds = std::ceil(tiles * s / 256.0);
+    double t = rounds * (np * std::ceil((double)kt / s) + 3.0) * t_kt;
+    if (s > 1) t += (double)d.batch * s * d.M * d.N * 8.0 / 4.5e12 + 4e-6;
+    if (t < best * 0.97) { best = t; best_s = s; }
+  }
+  return best_s;
+}
+
 hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, hipStream_t st) {
   PParams p;
   p.g = g;
@@ -236,6 +467,20 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   p.npairs = n;
   p.npairs0 = d.nB < T ? d.nB : T;  // pairs with i == 0
   if (!p.dyn) p.npairs0 = n;
+  p.pab = 0;
+  for (int i = 0; i < n; ++i) p.pab |= (p.pa[i] | p.pb[i] << 2) << (4 * i);
+  if (gemm_bf16_wide(d)) {
+    p.g.ntm = (d.M + WT - 1) / WT;
+    p.g.ntn = (d.N + WT - 1) / WT;
+    switch (epi) {
+      case EPI_STORE: return launch_wide<EPI_STORE>(p, d.at, d.bt, st);
+      case EPI_ACT: return launch_wide<EPI_ACT>(p, d.at, d.bt, st);
+      case EPI_DACT: return launch_wide<EPI_DACT>(p, d.at, d.bt, st);
+      case EPI_BCE: return launch_wide<EPI_BCE>(p, d.at, d.bt, st);
+      case EPI_SIGMOID: return launch_wide<EPI_SIGMOID>(p, d.at, d.bt, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (epi) {
     case EPI_STORE: return launch_var<EPI_STORE>(p, d.at, d.bt, d.variant, st);
     case EPI_ACT: return launch_var<EPI_ACT>(p, d.at, d.bt, d.variant, st);

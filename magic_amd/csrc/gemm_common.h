@@ -50,11 +50,12 @@ __device__ __forceinline__ void store_planes(unsigned short* cp, long long pc, i
   }
 }
 
-// logical tile of this workgroup
+// logical tile of this workgroup (TBM x TBN tiles)
 struct Tile {
   int z, bi, si, m0, n0, nt, ks, ke;
 };
-__device__ __forceinline__ Tile tile_of(const Params& p, bool remap) {
+template <int TBM, int TBN>
+__device__ __forceinline__ Tile tile_of_t(const Params& p, bool remap) {
   Tile t;
   const int tiles = p.ntm * p.ntn;
   const int nwg = tiles * p.batch * p.split;
@@ -65,37 +66,42 @@ __device__ __forceinline__ Tile tile_of(const Params& p, bool remap) {
   t.nt = rem - mt * p.ntn;
   t.bi = t.z / p.split;
   t.si = t.z - t.bi * p.split;
-  t.m0 = mt * BM;
-  t.n0 = t.nt * BN;
+  t.m0 = mt * TBM;
+  t.n0 = t.nt * TBN;
   t.ks = t.si * p.kchunk;
   t.ke = min(p.K, t.ks + p.kchunk);
   return t;
 }
+__device__ __forceinline__ Tile tile_of(const Params& p, bool remap) {
+  return tile_of_t<BM, BN>(p, remap);
+}
 
-// Epilogue over the 2x2 32x32 accumulators of this wave.
-// C/D layout of a 32x32 MFMA: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
-// `red` must be >= 2*BM floats of LDS no longer used by the main loop (BCE only).
-template <int EPI>
-__device__ __forceinline__ void epilogue(const Params& p, const Tile& t, f32x16 (&acc)[2][2],
-                                         float* red) {
+// Epilogue over this wave's MI x NI 32x32 accumulators; the wave owns rows
+// [m0 + wm*MI*32, +MI*32) and columns [n0 + wn*NI*32, +NI*32) of a TBM-row tile whose
+// columns are split over NWN waves. C/D layout of a 32x32 MFMA:
+// col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5).
+// BCE: `red` >= NWN*TBM floats of LDS no longer read by the main loop; the row partials are
+// written per 128-column block (rowpart[row][N/128 blocks], gemm_bce_nblk) whatever the tile.
+template <int EPI, int MI, int NI, int TBM, int NWN>
+__device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x16 (&acc)[MI][NI],
+                                           float* red, int wm, int wn) {
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int lane = tid & 63;
   const int fr = lane & 31, fk = lane >> 5;
   float* __restrict__ C = p.C + (size_t)t.z * p.sC;  // z = bi*split + si (slab) or bi (split==1)
   unsigned short* cp = p.epi.cp ? p.epi.cp + (size_t)t.z * p.sC : nullptr;
-  const int rbase = t.m0 + wm * 64 + 4 * fk;
-  const int cbase = t.n0 + wn * 64 + fr;
+  const int rbase = t.m0 + wm * MI * 32 + 4 * fk;
+  const int cbase = t.n0 + wn * NI * 32 + fr;
   if constexpr (EPI == EPI_BCE) {
     const GemmEpi& e = p.epi;
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
+    for (int mi = 0; mi < MI; ++mi) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = rbase + mi * 32 + (r & 3) + 8 * (r >> 2);
         float rs = 0.f;
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
+        for (int ni = 0; ni < NI; ++ni) {
           const int col = cbase + ni * 32;
           if (row < p.M && col < p.N) {
             const float yv = sigmoid_f(acc[mi][ni][r]);
@@ -113,22 +119,32 @@ __device__ __forceinline__ void epilogue(const Params& p, const Tile& t, f32x16 
         }
 #pragma unroll
         for (int off = 16; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
-        if (fr == 0) red[wn * BM + (row - t.m0)] = rs;  // lanes 0 and 32
+        if (fr == 0) red[wn * TBM + (row - t.m0)] = rs;  // lanes 0 and 32
       }
     }
     __syncthreads();
-    if (tid < BM && t.m0 + tid < p.M) {
-      e.rowpart[(size_t)(t.m0 + tid) * p.ntn + t.nt] = -(red[tid] + red[BM + tid]);
+    constexpr int WPB = 128 / (NI * 32);  // waves per 128-column block
+    constexpr int NBT = NWN / WPB;        // 128-column blocks per tile
+    const int nblk = (p.N + 127) / 128;
+    for (int i = tid; i < NBT * TBM; i += blockDim.x) {
+      const int b = i / TBM, r = i - b * TBM;
+      const int gb = t.nt * NBT + b;
+      if (gb < nblk && t.m0 + r < p.M) {
+        float s_ = 0.f;
+#pragma unroll
+        for (int w = 0; w < WPB; ++w) s_ += red[(b * WPB + w) * TBM + r];
+        e.rowpart[(size_t)(t.m0 + r) * nblk + gb] = -s_;
+      }
     }
   } else {
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
+    for (int mi = 0; mi < MI; ++mi) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = rbase + mi * 32 + (r & 3) + 8 * (r >> 2);
         if (row >= p.M) continue;
 #pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
+        for (int ni = 0; ni < NI; ++ni) {
           const int col = cbase + ni * 32;
           if (col >= p.N) continue;
           float v = acc[mi][ni][r];
@@ -144,6 +160,14 @@ __device__ __forceinline__ void epilogue(const Params& p, const Tile& t, f32x16 
       }
     }
   }
+}
+
+// the 128x128-tile kernels: 4 waves in 2x2, each 2x2 accumulators
+template <int EPI>
+__device__ __forceinline__ void epilogue(const Params& p, const Tile& t, f32x16 (&acc)[2][2],
+                                         float* red) {
+  const int wave = threadIdx.x >> 6;
+  epilogue_g<EPI, 2, 2, BM, 2>(p, t, acc, red, wave >> 1, wave & 1);
 }
 
 }  // namespace gemm

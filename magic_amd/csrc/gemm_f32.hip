@@ -250,6 +250,7 @@ int gemm_bce_nblk(int N) { return (N + BN - 1) / BN; }
 
 int gemm_plan_split(const GemmDesc& d, size_t max_ws) {
   if (d.epi.mode == EPI_BCE || d.epi.mode == EPI_SIGMOID) return 1;
+  if (gemm_bf16_wide(d)) return gemm_bf16_wide_split(d, max_ws);
   const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
   const long long tiles = (long long)ntm * ntn * d.batch;
   const int ktiles = (d.K + BK - 1) / BK;
@@ -288,8 +289,9 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   p.epi = d.epi;
   const int split = d.split > 0 ? d.split : gemm_plan_split(d, ws ? ws_elems : 0);
   p.split = split;
-  const int ktiles = (d.K + BK - 1) / BK;
-  p.kchunk = ((ktiles + split - 1) / split) * BK;
+  const int kb = d.prec == GEMM_F32 ? BK : 64;  // k-tile of the kernel that runs
+  const int ktiles = (d.K + kb - 1) / kb;
+  p.kchunk = ((ktiles + split - 1) / split) * kb;
   if (split == 1) {
     p.C = d.C; p.ldc = d.ldc; p.sC = d.sC;
     if (d.prec != GEMM_F32) return gemm_bf16_launch(p, d, d.epi.mode, st);

@@ -55,7 +55,9 @@ struct mvae_ctx {
   float *ms = nullptr, *z = nullptr, *a1 = nullptr, *a2 = nullptr, *du = nullptr;
   float *rowpart = nullptr, *rowvals = nullptr, *dist = nullptr, *draw = nullptr, *losses = nullptr;
   float *colsq = nullptr, *coldot = nullptr, *cspart = nullptr, *eps = nullptr;
-  float *dzd2 = nullptr, *dzd1 = nullptr, *dzdec = nullptr, *dhead = nullptr, *dz[2] = {nullptr, nullptr};
+  float *dzd2 = nullptr, *dzd1 = nullptr, *dzdec = nullptr, *dhead = nullptr;
+  std::vector<float*> dzl;  // dZ of every encoder layer [4B][lddz] (all live until its wgrad)
+  int enc_part1 = 0;        // bwd_enc[0, enc_part1): dgrad chain + layer-0 wgrad
   float* zgen = nullptr;
   float* ws = nullptr;
   size_t ws_elems = 0;
@@ -228,38 +230,42 @@ static void build_schedule(mvae_ctx* c) {
                           c->ld_d1, false, g1 + c->v1.off, c->v1.ld));
   c->bwd_dec.push_back(gd(B, L, c->d0, c->dzd1, c->ld_d1, false, th + c->v1.off, c->v1.ld, true,
                           c->dzdec, L));
-  // ---- encoder backward: g1 over rows [rot|lock], g2 over [lock|key] (batched GEMMs)
+  // ---- encoder backward: g1 over rows [rot|lock], g2 over [lock|key] (batched GEMMs).
+  // Part 1 runs the dgrad chain (head -> layer 1) and then the big layer-0 weight gradient;
+  // part 2 the small weight gradients of the head and hidden layers. Each part ends with a
+  // set of finished gradient ranges (the all-reduce buckets of mvae_grad_range), so a data-
+  // parallel host overlaps the decoder and layer-0 all-reduces with the remaining work.
   c->bwd_enc.clear();
-  {
-    GemmDesc w = gd(c->head.K + 1, 2 * L, 2 * B, c->H[n - 1], c->ldh[n - 1], true, c->dhead, c->ld_dh,
-                    false, g1 + c->head.off, c->head.ld);
-    w.batch = 2; w.sA = (long long)B * c->ldh[n - 1]; w.sB = (long long)2 * B * c->ld_dh; w.sC = n_all;
-    c->bwd_enc.push_back(w);
-    c->bwd_enc_r.push_back(region(c, "head_bwd_w"));
-    GemmDesc d = gd(4 * B, c->head.K, 2 * L, c->dhead, c->ld_dh, false, th + c->head.off, c->head.ld, true,
-                    c->dz[(n - 1) & 1], c->lddz, EPI_DACT);
-    d.epi.act = act; d.epi.aux = c->H[n - 1]; d.epi.ld_aux = c->ldh[n - 1];
+  c->bwd_enc_r.clear();
+  auto dgrad = [&](int i) {  // dZ_{i-1} = (dZ_i W_i^T) * act'(H_{i-1}); i == n: the head
+    const bool head = i == n;
+    const Block& blk = head ? c->head : c->enc[i];
+    const float* src = head ? c->dhead : c->dzl[i];
+    const int lds = head ? c->ld_dh : c->lddz;
+    GemmDesc d = gd(4 * B, blk.K, blk.N, src, lds, false, th + blk.off, blk.ld, true, c->dzl[i - 1],
+                    c->lddz, EPI_DACT);
+    d.epi.act = act; d.epi.aux = c->H[i - 1]; d.epi.ld_aux = c->ldh[i - 1];
     d.epi.remap_split = 2 * B; d.epi.remap_shift = B;
     c->bwd_enc.push_back(d);
-    c->bwd_enc_r.push_back(region(c, "head_bwd_d"));
-  }
-  for (int i = n - 1; i >= 0; --i) {
+    c->bwd_enc_r.push_back(region(c, head ? std::string("head_bwd_d") : "enc_bwd_d_" + std::to_string(i)));
+  };
+  auto wgrad = [&](int i) {  // [W_i; b_i] gradients (g1 and g2 as one batch-2 GEMM); i == n: head
+    const bool head = i == n;
+    const Block& blk = head ? c->head : c->enc[i];
     const float* A = i == 0 ? c->xs : c->H[i - 1];
     const int lda = i == 0 ? c->ldx : c->ldh[i - 1];
-    GemmDesc w = gd(c->enc[i].K + 1, c->enc[i].N, 2 * B, A, lda, true, c->dz[i & 1], c->lddz, false,
-                    g1 + c->enc[i].off, c->enc[i].ld);
-    w.batch = 2; w.sA = (long long)B * lda; w.sB = (long long)2 * B * c->lddz; w.sC = n_all;
+    const float* src = head ? c->dhead : c->dzl[i];
+    const int lds = head ? c->ld_dh : c->lddz;
+    GemmDesc w = gd(blk.K + 1, blk.N, 2 * B, A, lda, true, src, lds, false, g1 + blk.off, blk.ld);
+    w.batch = 2; w.sA = (long long)B * lda; w.sB = (long long)2 * B * lds; w.sC = n_all;
     c->bwd_enc.push_back(w);
-    c->bwd_enc_r.push_back(region(c, "enc_bwd_w_" + std::to_string(i)));
-    if (i > 0) {
-      GemmDesc d = gd(4 * B, c->enc[i].K, c->enc[i].N, c->dz[i & 1], c->lddz, false,
-                      th + c->enc[i].off, c->enc[i].ld, true, c->dz[(i - 1) & 1], c->lddz, EPI_DACT);
-      d.epi.act = act; d.epi.aux = c->H[i - 1]; d.epi.ld_aux = c->ldh[i - 1];
-      d.epi.remap_split = 2 * B; d.epi.remap_shift = B;
-      c->bwd_enc.push_back(d);
-      c->bwd_enc_r.push_back(region(c, "enc_bwd_d_" + std::to_string(i)));
-    }
-  }
+    c->bwd_enc_r.push_back(region(c, head ? std::string("head_bwd_w") : "enc_bwd_w_" + std::to_string(i)));
+  };
+  for (int i = n; i >= 1; --i) dgrad(i);
+  wgrad(0);
+  c->enc_part1 = (int)c->bwd_enc.size();
+  wgrad(n);
+  for (int i = n - 1; i >= 1; --i) wgrad(i);
   for (const char* nm : {"deinterleave", "eps_rng", "latent_fwd", "colsq", "metric_loss", "coldot",
                          "latent_bwd", "adam"})
     region(c, nm);
@@ -397,8 +403,8 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   ALLOC(c->dzd1, B * c->ld_d1);
   ALLOC(c->dzdec, B * L);
   ALLOC(c->dhead, 4 * B * c->ld_dh);
-  ALLOC(c->dz[0], 4 * B * c->lddz);
-  ALLOC(c->dz[1], 4 * B * c->lddz);
+  c->dzl.resize(c->nenc);
+  for (int i = 0; i < c->nenc; ++i) ALLOC(c->dzl[i], 4 * B * c->lddz);
   // constant ones columns (bias folding)
   hipError_t e = ones_column(c->xs, c->ldx, c->D, 3 * (int)B);
   for (int i = 0; e == hipSuccess && i < c->nenc; ++i) e = ones_column(c->H[i], c->ldh[i], cfg->enc[i], 3 * (int)B);
@@ -438,8 +444,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     if (e == hipSuccess) e = add(c->dzd2, B * c->ld_d2);
     if (e == hipSuccess) e = add(c->dzd1, B * c->ld_d1);
     if (e == hipSuccess) e = add(c->dhead, 4 * B * c->ld_dh);
-    if (e == hipSuccess) e = add(c->dz[0], 4 * B * c->lddz);
-    if (e == hipSuccess) e = add(c->dz[1], 4 * B * c->lddz);
+    for (int i = 0; e == hipSuccess && i < c->nenc; ++i) e = add(c->dzl[i], 4 * B * c->lddz);
     if (e == hipSuccess && c->np == 3) e = dalloc(c, reinterpret_cast<float**>(&c->dyn), 4);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
@@ -664,24 +669,58 @@ extern "C" int mvae_metric(mvae_ctx* ctx, const float* areas, void* stream) {
   return MVAE_OK;
 }
 
-extern "C" int mvae_backward(mvae_ctx* ctx, void* stream) {
+// Backward in three parts (phase 2 -> 4 -> 5 -> 3); after part k the ranges
+// mvae_grad_range(ctx, k, i, ...) hold final (rank-local) gradients.
+extern "C" int mvae_backward_part(mvae_ctx* ctx, int part, void* stream) {
   if (!ctx) return MVAE_EINVAL;
-  if (ctx->phase != 2) return fail(ctx, MVAE_ESTATE, "mvae_backward before mvae_metric");
+  const int need = part == 0 ? 2 : (part == 1 ? 4 : 5);
+  if (part < 0 || part > 2) return fail(ctx, MVAE_EINVAL, "backward part must be 0, 1 or 2");
+  if (ctx->phase != need) return fail(ctx, MVAE_ESTATE, "mvae_backward_part out of order");
   hipStream_t st = (hipStream_t)stream;
   auto c = ctx;
   int rc;
-  for (size_t i = 0; i < c->bwd_dec.size(); ++i)
-    if ((rc = run(c, c->bwd_dec[i], st, c->bwd_dec_r[i]))) return rc;
-  {
-    TIMED("latent_bwd");
-    MV_CHECK(launch_latent_bwd(c->z, c->ldz, c->ms, c->eps, c->dzdec, c->draw, c->colsq, c->coldot,
-                               c->B, c->L, c->cfg.metric, c->cfg.deform_weight, c->inv_bg, c->dhead,
-                               c->ld_dh, planes_of(c, c->dhead), st));
+  if (part == 0) {
+    for (size_t i = 0; i < c->bwd_dec.size(); ++i)
+      if ((rc = run(c, c->bwd_dec[i], st, c->bwd_dec_r[i]))) return rc;
+    ctx->phase = 4;
+  } else if (part == 1) {
+    {
+      TIMED("latent_bwd");
+      MV_CHECK(launch_latent_bwd(c->z, c->ldz, c->ms, c->eps, c->dzdec, c->draw, c->colsq, c->coldot,
+                                 c->B, c->L, c->cfg.metric, c->cfg.deform_weight, c->inv_bg, c->dhead,
+                                 c->ld_dh, planes_of(c, c->dhead), st));
+    }
+    for (int i = 0; i < c->enc_part1; ++i)
+      if ((rc = run(c, c->bwd_enc[i], st, c->bwd_enc_r[i]))) return rc;
+    ctx->phase = 5;
+  } else {
+    for (size_t i = c->enc_part1; i < c->bwd_enc.size(); ++i)
+      if ((rc = run(c, c->bwd_enc[i], st, c->bwd_enc_r[i]))) return rc;
+    ctx->phase = 3;
   }
-  for (size_t i = 0; i < c->bwd_enc.size(); ++i)
-    if ((rc = run(c, c->bwd_enc[i], st, c->bwd_enc_r[i]))) return rc;
-  ctx->phase = 3;
   return MVAE_OK;
+}
+
+extern "C" int mvae_backward(mvae_ctx* ctx, void* stream) {
+  if (!ctx) return MVAE_EINVAL;
+  if (ctx->phase != 2) return fail(ctx, MVAE_ESTATE, "mvae_backward before mvae_metric");
+  int rc;
+  for (int part = 0; part < 3; ++part)
+    if ((rc = mvae_backward_part(ctx, part, stream))) return rc;
+  return MVAE_OK;
+}
+
+extern "C" int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* count) {
+  if (!ctx || !ptr || !count) return MVAE_EINVAL;
+  const size_t l1 = ctx->nenc > 1 ? ctx->enc[1].off : ctx->head.off;  // end of the layer-0 block
+  float* g1 = ctx->grads;
+  float* g2 = ctx->grads + ctx->n_all;
+  if (part == 0 && index == 0) { *ptr = g1 + ctx->n_enc; *count = ctx->n_all - ctx->n_enc; return MVAE_OK; }
+  if (part == 1 && index == 0) { *ptr = g1; *count = l1; return MVAE_OK; }
+  if (part == 1 && index == 1) { *ptr = g2; *count = l1; return MVAE_OK; }
+  if (part == 2 && index == 0) { *ptr = g1 + l1; *count = ctx->n_enc - l1; return MVAE_OK; }
+  if (part == 2 && index == 1) { *ptr = g2 + l1; *count = ctx->n_enc - l1; return MVAE_OK; }
+  return MVAE_EINVAL;
 }
 
 extern "C" int mvae_adam(mvae_ctx* ctx, void* stream) {
@@ -785,11 +824,12 @@ extern "C" int mvae_generate(mvae_ctx* ctx, const float* zin, int n, float* y_ou
 extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int at, const float* Bm,
                                int ldb, int bt, float* Cm, int ldc, int epi, int act, const float* aux,
                                int ld_aux, void* stream) {
-  if ((epi & 15) == EPI_BCE || epi < 0 || (epi & 15) > EPI_SIGMOID || (epi >> 4) > 2)
+  if ((epi & 15) == EPI_BCE || epi < 0 || (epi & 15) > EPI_SIGMOID || ((epi >> 4) & 15) > 2)
     return fail(nullptr, MVAE_EINVAL, "bad epilogue");
   hipStream_t st = (hipStream_t)stream;
   GemmDesc d = gd(M, N, K, A, lda, at != 0, Bm, ldb, bt != 0, Cm, ldc, epi & 15);
-  d.prec = epi >> 4;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
+  d.prec = (epi >> 4) & 15;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
+  d.variant = (epi >> 8) & 15;
   d.epi.act = act;
   d.epi.aux = aux;
   d.epi.ld_aux = ld_aux;
@@ -873,10 +913,13 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
                                void* stream, float* avg_ms) {
   if (M <= 0 || N <= 0 || K <= 0 || iters <= 0 || !avg_ms || batch <= 0) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  const size_t na = (size_t)M * K * batch, nb = (size_t)K * N * batch, nc = (size_t)M * N * batch;
+  // operand rows padded to 8 elements (16 B), as the step's buffers are
+  const int lda = ((at ? M : K) + 7) & ~7, ldb = ((bt ? K : N) + 7) & ~7;
+  const size_t sa = (size_t)(at ? K : M) * lda, sb = (size_t)(bt ? N : K) * ldb;
+  const size_t na = sa * batch, nb = sb * batch, nc = (size_t)M * N * batch;
   float *A = nullptr, *Bm = nullptr, *Cm = nullptr, *ws = nullptr;
-  GemmDesc d = gd(M, N, K, nullptr, at ? M : K, at != 0, nullptr, bt ? K : N, bt != 0, nullptr, N);
-  d.batch = batch; d.sA = (long long)M * K; d.sB = (long long)K * N; d.sC = (long long)M * N;
+  GemmDesc d = gd(M, N, K, nullptr, lda, at != 0, nullptr, ldb, bt != 0, nullptr, N);
+  d.batch = batch; d.sA = (long long)sa; d.sB = (long long)sb; d.sC = (long long)M * N;
   d.variant = variant & 15;
   d.prec = variant >> 4;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
   unsigned short* planes = nullptr;

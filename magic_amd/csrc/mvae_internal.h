@@ -67,6 +67,9 @@ size_t gemm_workspace_elems(const GemmDesc& d);
 hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t st);
 namespace gemm { struct Params; }
 hipError_t gemm_bf16_launch(const gemm::Params& p, const GemmDesc& d, int epi, hipStream_t st);
+// bf16-plane GEMMs: the 256x256 wide kernel serves d? (shape/alignment), and its split-K plan
+bool gemm_bf16_wide(const GemmDesc& d);
+int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws);
 // Number of column blocks the BCE epilogue writes per row (rowpart's inner dim).
 int gemm_bce_nblk(int N);
 

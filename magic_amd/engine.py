@@ -177,6 +177,26 @@ class Engine:
     def backward(self):
         self._check(self.lib.mvae_backward(self.ctx, self.stream))
 
+    N_BACKWARD_PARTS = 3
+
+    def backward_part(self, part: int):
+        """Part ``part`` (0, 1, 2 in order) of ``backward``; see ``grad_ranges``."""
+        self._check(self.lib.mvae_backward_part(self.ctx, part, self.stream))
+
+    def grad_ranges(self, part: int):
+        """Views of ``grads`` that are final once ``backward_part(part)`` has run."""
+        base = self.grads.data_ptr()
+        out = []
+        for i in range(8):
+            p = C.c_void_p()
+            n = C.c_size_t()
+            if self.lib.mvae_grad_range(self.ctx, part, i, C.byref(p), C.byref(n)) != 0:
+                break
+            off = (p.value - base) // 4
+            if n.value:
+                out.append(self.grads[off:off + n.value])
+        return out
+
     def adam(self):
         self._check(self.lib.mvae_adam(self.ctx, self.stream))
 

@@ -9,8 +9,10 @@ Per step and rank (``world`` ranks, local batch B, global batch N*B):
                                        the GLOBAL batch (``8c/vae.py:449-450``)
   metric(areas_local)
   all_reduce(coldot) [cosine only]     L floats: sum_b draw_b n_lock n_key (global)
-  backward()
-  all_reduce(grads)                    ONE bucket [g1 | g2] (RCCL over xGMI on MI355X)
+  backward()                           in three parts; the gradient ranges each part
+  all_reduce(grads)                    finishes (decoder; layer-0 g1/g2; the rest) are
+                                       all-reduced asynchronously (RCCL over xGMI on
+                                       MI355X) while the later parts run, then waited on
   adam()                               identical on every rank -> replicas stay bitwise equal
   all_reduce(losses) (optional)        5 floats, for logging / the NaN guard
 
@@ -28,8 +30,11 @@ class DataParallelStep:
     ``colsq``, ``coldot``, ``grads``, ``losses`` (the HIP ``Engine``; tests also drive a
     CPU stand-in built on the oracle)."""
 
-    def __init__(self, engine, group=None, reduce_losses: bool = True):
+    def __init__(self, engine, group=None, reduce_losses: bool = True, overlap: bool = True):
         self.e = engine
+        # bucketed all-reduce overlapped with the rest of the backward (engines exposing
+        # backward_part/grad_ranges); otherwise one bucket after the whole backward
+        self.overlap = overlap and hasattr(engine, "backward_part")
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.reduce_losses = reduce_losses
@@ -50,8 +55,18 @@ class DataParallelStep:
         e.metric(areas)
         if self.cosine:
             self._ar(e.coldot)
-        e.backward()
-        self._ar(e.grads)
+        if self.world > 1 and self.overlap:
+            handles = []
+            for part in range(e.N_BACKWARD_PARTS):
+                e.backward_part(part)
+                for view in e.grad_ranges(part):
+                    handles.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group,
+                                                   async_op=True))
+            for h in handles:
+                h.wait()
+        else:
+            e.backward()
+            self._ar(e.grads)
         e.adam()
         if self.reduce_losses:
             self._ar(e.losses)

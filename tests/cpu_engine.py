@@ -47,6 +47,19 @@ class OracleEngine:
         flat = [g1[n].reshape(-1) for n in self.names1] + [g2[n].reshape(-1) for n in self.names2]
         self.grads.copy_(torch.from_numpy(np.concatenate(flat)))
 
+    # the HIP engine's three-part backward: here part 0 computes everything and the
+    # ranges are a fixed partition of ``grads`` released part by part (host-logic test)
+    N_BACKWARD_PARTS = 3
+
+    def backward_part(self, part):
+        if part == 0:
+            self.backward()
+
+    def grad_ranges(self, part):
+        n = self.grads.numel()
+        cuts = [0, n // 5, n // 2, n]
+        return [self.grads[cuts[part]:cuts[part + 1]]]
+
     def adam(self):
         g = self.grads.numpy()
         g1, g2, o = {}, {}, 0

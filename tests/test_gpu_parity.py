@@ -54,6 +54,40 @@ def test_gemm_layouts(at, bt, M, N, K, prec):
     assert err <= bound, (err, bound)
 
 
+def _padded(rows, cols, g):
+    """[rows, cols] random operand inside a zero-padded [rows, round8(cols)] buffer (the
+    step's row strides are multiples of 8 elements with zero padding)."""
+    ld = (cols + 7) // 8 * 8
+    buf = torch.zeros(rows, ld, device="cuda")
+    buf[:, :cols] = torch.randn(rows, cols, device="cuda", generator=g)
+    return buf
+
+
+@pytest.mark.parametrize("prec", [2, 1], ids=["f32x", "bf16"])
+@pytest.mark.parametrize("at,bt", [(0, 0), (1, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("M,N,K,variant", [(256, 256, 64, 3), (300, 517, 1001, 3), (1000, 600, 4099, 0),
+                                           (513, 260, 130, 0), (40, 70, 200, 3)])
+def test_gemm_wide_kernel(at, bt, M, N, K, variant, prec):
+    """The 256x256 LDS-DMA bf16 kernel (variant 3 forces it; 0 lets the planner pick it for
+    M, N >= 256) on every layout, ragged edges and split-K, against float64."""
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(M * 5 + N * 11 + K)
+    A = _padded(K, M, g) if at else _padded(M, K, g)
+    Bm = _padded(N, K, g) if bt else _padded(K, N, g)
+    C = torch.full((M, N), float("nan"), device="cuda")
+    rc = lib.mvae_debug_gemm(M, N, K, A.data_ptr(), A.shape[1], at, Bm.data_ptr(), Bm.shape[1], bt,
+                             C.data_ptr(), N, (prec << 4) | (variant << 8), 0, None, 0,
+                             torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, lib.mvae_last_error(None)
+    Ad = (A[:, :M].double().T if at else A[:, :K].double())
+    Bd = (Bm[:, :K].double().T if bt else Bm[:, :N].double())
+    ref = Ad @ Bd
+    err = (C.double() - ref).abs().max().item()
+    mag = (Ad.abs() @ Bd.abs()).max().item()
+    bound = (2e-6 if prec != 1 else 1e-2) * mag + 1e-6
+    assert err <= bound, (err, bound)
+
+
 def test_gemm_f32x_exact_operand_takes_one_term():
     """A binary operand (exact in bf16) through the split kernel: identical result class."""
     lib = _lib.load()
@@ -217,6 +251,46 @@ def test_determinism_bitwise():
             np.testing.assert_array_equal(a, b)
         for k in outs[0][2]:
             np.testing.assert_array_equal(outs[0][2][k], outs[1][2][k])
+    finally:
+        eng.close()
+
+
+@pytest.mark.parametrize("n_enc", [1, 3])
+def test_backward_parts_match_backward(n_enc):
+    """backward_part(0..2) == backward bitwise; the released ranges tile g1 and the encoder
+    part of g2 exactly once (the data-parallel all-reduce buckets)."""
+    cfg = preset("8c", image_size=30, batch=96).replace(enc=(300, 200, 120)[:n_enc], latent=24)
+    eng = _engine(cfg)
+    try:
+        P = make_params(cfg)
+        X, areas, eps = make_inputs(cfg, cfg.batch)
+        x, a, e = to_dev(X), to_dev(areas), to_dev(eps)
+        eng.load_params(P)
+        eng.forward(x, e)
+        eng.metric(a)
+        eng.backward()
+        ref = eng.grads.clone()
+        eng.forward(x, e)
+        eng.metric(a)
+        seen = torch.zeros(eng.grads.numel(), dtype=torch.int32, device=eng.grads.device)
+        base = eng.grads.data_ptr()
+        end = 0
+        for part in range(eng.N_BACKWARD_PARTS):
+            eng.backward_part(part)
+            for v in eng.grad_ranges(part):
+                off = (v.data_ptr() - base) // 4
+                seen[off:off + v.numel()] += 1
+                end = max(end, off + v.numel())
+        torch.cuda.synchronize()
+        n_all = eng.grads.numel() // 2
+        n_enc = end - n_all  # padded encoder extent of g2
+        assert n_enc >= sum(t.numel() for k, t in eng.params().items() if k.startswith("enc_"))
+        assert torch.equal(eng.grads[:end], ref[:end])
+        s_ = seen.cpu().numpy()
+        assert (s_[:n_all] == 1).all() and (s_[n_all:n_all + n_enc] == 1).all()
+        assert (s_[n_all + n_enc:] == 0).all()
+        with pytest.raises(_lib.MVAEError):
+            eng.backward_part(1)  # out of order
     finally:
         eng.close()
 

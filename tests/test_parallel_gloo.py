@@ -32,7 +32,7 @@ def _inputs(cfg, B):
     return torch.from_numpy(X), torch.from_numpy(areas), torch.from_numpy(eps)
 
 
-def _worker(rank, world, port, metric, recip, q):
+def _worker(rank, world, port, metric, recip, q, overlap=True):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     cfg = _cfg(metric, recip)
@@ -42,7 +42,7 @@ def _worker(rank, world, port, metric, recip, q):
     P = O.init_params(oc, seed=0, dtype=np.float64)
     X, A, E = _inputs(cfg, full_B)
     eng = OracleEngine(cfg, P)
-    step = DataParallelStep(eng)
+    step = DataParallelStep(eng, overlap=overlap)
     for _ in range(2):
         losses = step.step(shard_rows(X, rank, world), shard_rows(A, rank, world),
                            E[:, rank * cfg.batch:(rank + 1) * cfg.batch].contiguous())
@@ -58,13 +58,14 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("metric,recip", [("sqdiff", True), ("cosine", False), ("cosine", True)])
-def test_dp2_equals_single_process(metric, recip):
+@pytest.mark.parametrize("metric,recip,overlap", [("sqdiff", True, True), ("cosine", False, True),
+                                                  ("cosine", True, True), ("cosine", True, False)])
+def test_dp2_equals_single_process(metric, recip, overlap):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, metric, recip, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, metric, recip, q, overlap)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict((r, (P, l)) for r, P, l in (q.get(timeout=240) for _ in range(world)))
