@@ -27,6 +27,7 @@ import torch.distributed as dist
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
+from magic_amd import _lib  # noqa: E402
 from magic_amd.config import baseline_config  # noqa: E402
 
 METRIC = "shape-pairs/sec/GPU (train step) + overlap-MSE, 100×100 pairs, 1/2/4/8 GPUs"
@@ -182,20 +183,31 @@ def main():
             ms_avg = gemms[dom][0] / gemms[dom][1]
             flops = region_flops(cfg, dom)
             achieved = flops / (ms_avg * 1e-3) / 1e12
-            # f32x issues 3 bf16 MFMAs per exact-bf16 x fp32 product (6 for fp32 x fp32): its
-            # algorithmic fp32 FLOPs are priced against the fp32 peak it replaces
             peak = BF16_MFMA_PEAK_TFLOPS if cfg.precision == "bf16" else F32_MFMA_PEAK_TFLOPS
+            extra = {}
+            if cfg.precision == "f32x":
+                # the exact 3-term split runs the plane pairs (i, j), i + j < 3, as bf16 MFMA
+                # work: 6 pairs, or 3 when the A operand (the pixels) is exact in bf16. Its
+                # algorithm's FLOPs are pairs x 2MNK at the bf16 peak; the fp32-equivalent
+                # rate (2MNK / time) is reported beside it.
+                dyn = int(eng.buffer(_lib.BUF_DYN).view(torch.int32).item())
+                pairs = 3 if dom in ("enc_fwd_0", "enc_bwd_w_0") and dyn == 0 else 6
+                extra = {"fp32_equivalent_tflops": round(achieved, 2), "bf16_plane_pairs": pairs}
+                achieved *= pairs
+                flops *= pairs
+                peak = BF16_MFMA_PEAK_TFLOPS
             traffic = None
             try:
                 with open(args.traffic_json) as f:
                     tj = json.load(f)
-                if tj.get("config") == args.config and dom in tj.get("regions", {}):
+                if (tj.get("config") == args.config and tj.get("precision") == cfg.precision
+                        and dom in tj.get("regions", {})):
                     traffic = tj["regions"][dom]["hbm_bytes_per_launch"]
             except (OSError, ValueError):
                 pass
             roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
                         "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                        "kernel": dom, "flops_per_launch": flops, "avg_ms": round(ms_avg, 4)}
+                        "kernel": dom, "flops_per_launch": flops, "avg_ms": round(ms_avg, 4), **extra}
             total_gemm_ms = sum(v[0] for v in gemms.values()) / args.steps
             gemm_flops = sum(region_flops(cfg, k) * v[1] for k, v in gemms.items()) / args.steps
             print(f"[bench] GEMM time/step {total_gemm_ms:.3f} ms, {gemm_flops / total_gemm_ms / 1e9:.1f} TFLOP/s "

@@ -94,7 +94,10 @@ enum {
   MVAE_BUF_DIST = 6,     /* float[B]: distance of the last forward                      */
   MVAE_BUF_GRADS_DEC = 7,/* decoder slice of g1 (ready first in mvae_backward)         */
   MVAE_BUF_DEAD = 8,     /* the never-trained decoder log-sigma variables               */
-  MVAE_BUF_EPS = 9       /* float[3,B,L]: eps of the last forward (given or generated)  */
+  MVAE_BUF_EPS = 9,      /* float[3,B,L]: eps of the last forward (given or generated)  */
+  MVAE_BUF_DYN = 10      /* int32[1] (count 1): nonzero when the last batch's pixels are
+                            not all exact in bf16 (f32x mode: the layer-0 GEMMs then run
+                            all 6 plane pairs instead of 3); 0 in other modes             */
 };
 
 int mvae_abi_version(void);
@@ -162,7 +165,7 @@ int mvae_timing_reset(mvae_ctx* ctx);
  * 1 act (act: 0 tanh, 1 elu), 2 C = acc * act'(aux), 4 sigmoid; epi | (prec << 4) |
  * (variant << 8) selects the arithmetic (MVAE_PREC_*) and kernel (0 auto, 3 the 256x256
  * bf16 kernel, 4 the 128x128 one). Workspace is allocated and freed inside
- * (synchronous; tests only). mvae_bench_gemm: variant | (prec << 4).                 */
+ * (synchronous; tests only). mvae_bench_gemm: variant | (prec << 4) | (epi << 8).    */
 int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, int variant, int iters,
                     void* stream, float* avg_ms);
 int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int at, const float* B, int ldb,

@@ -21,7 +21,7 @@ PREC = {"f32": 0, "bf16": 1, "f32x": 2}
 
 KIND_PARAM, KIND_GRAD1, KIND_GRAD2, KIND_M1, KIND_V1, KIND_M2, KIND_V2 = range(7)
 (BUF_PARAMS, BUF_GRADS, BUF_ADAM, BUF_LOSSES, BUF_COLSQ, BUF_COLDOT, BUF_DIST, BUF_GRADS_DEC,
- BUF_DEAD, BUF_EPS) = range(10)
+ BUF_DEAD, BUF_EPS, BUF_DYN) = range(11)
 
 
 class MVAELibraryError(RuntimeError):

@@ -211,32 +211,36 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16p_kernel(PParams pp) {
 // zero page, so partial tiles need no masking; rows past the end of a k-contiguous operand
 // are clamped (their outputs are not stored). Requires every ld, batch and plane stride and
 // the K padding [K, round8(K)) of k-contiguous operands to be zero-filled multiples of 8.
-constexpr int WT = 256, WNT = 512, WBK = 64;
-constexpr int WIMG = WT * WBK;  // bf16 elements per operand image
+constexpr int WT = 256, WNT = 512;
 
 __device__ __attribute__((aligned(16))) int4 g_zero16[1];
 typedef __attribute__((address_space(3))) short lds_short;
 
-template <bool KC>
+// operand image of one k-tile (BK = 64 or 32): NG = BK/16 DMA instructions per thread
+template <bool KC, int BK>
 struct WLoad {
-  long long off[4];
-  int kc[4];
-  bool rv[4];
+  static constexpr int NG = BK / 16;
+  static constexpr int CPR = BK / 8;    // 16-B chunks per row of a k-contiguous image
+  static constexpr int RPB = 128 / BK;  // k-contiguous rows per 256-B bank row
+  long long off[NG];
+  int kc[NG];
+  bool rv[NG];
+  __device__ __forceinline__ static int swz(int row) { return (row / RPB) & (CPR - 1); }
   __device__ __forceinline__ void init(int ld, int r0, int nrows, int wave, int lane) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q0 = j * 8 + wave;  // 64-chunk group of this wave-instruction
+    for (int j = 0; j < NG; ++j) {
+      const int q = (j * 8 + wave) * 64 + lane;  // chunk this lane copies
       if constexpr (KC) {
-        const int row = q0 * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ ((row >> 1) & 7);
+        const int row = q / CPR;
+        const int c = (q % CPR) ^ swz(row);
         int gr = r0 + row;
         gr = gr < nrows ? gr : nrows - 1;
         off[j] = (long long)gr * ld + 8 * c;
         kc[j] = 8 * c;
         rv[j] = true;
       } else {
-        const int krow = q0 * 2 + (lane >> 5);
-        const int c = (lane & 31) ^ (4 * (krow & 3));
+        const int krow = q >> 5;
+        const int c = (q & 31) ^ (4 * (krow & 3));
         const int col = r0 + 8 * c;
         rv[j] = col < nrows;
         off[j] = (long long)krow * ld + col;
@@ -247,7 +251,7 @@ struct WLoad {
   __device__ __forceinline__ void issue(const unsigned short* __restrict__ g, int ld, int k0,
                                         int kend, short* img, int wave) const {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < NG; ++j) {
       const bool ok = rv[j] && k0 + kc[j] < kend;
       const unsigned short* src = KC ? g + off[j] + k0 : g + off[j] + (long long)k0 * ld;
       src = ok ? src : reinterpret_cast<const unsigned short*>(g_zero16);
@@ -259,13 +263,13 @@ struct WLoad {
   // fragment (8 consecutive k) of the 32-row block at rb, k16-step ks. The transposing reads
   // are inline asm: the builtin makes hipcc wait for every outstanding LDS-DMA (vmcnt(0))
   // before it, serialising the next tile's copy with this tile's MFMAs. Their results are
-  // waited for explicitly (wait_frags) before use.
+  // waited for explicitly (wait_lds) before use.
   __device__ __forceinline__ bf16x8 frag(const short* s, unsigned s_lds, int rb, int ks,
                                          int lane) const {
     if constexpr (KC) {
       const int row = rb + (lane & 31);
-      const int pos = (2 * ks + (lane >> 5)) ^ ((row >> 1) & 7);
-      const s16x8 v = *reinterpret_cast<const s16x8*>(s + row * WBK + pos * 8);
+      const int pos = (2 * ks + (lane >> 5)) ^ swz(row);
+      const s16x8 v = *reinterpret_cast<const s16x8*>(s + row * BK + pos * 8);
       return __builtin_bit_cast(bf16x8, v);
     } else {
       const int i = lane & 15, q = i >> 2, pp = i & 3;
@@ -281,7 +285,7 @@ struct WLoad {
   }
 };
 
-// wait until at most n LDS instructions are outstanding (n is a literal per instantiation)
+// wait until at most N LDS instructions are outstanding (N is a literal per instantiation)
 template <int N>
 __device__ __forceinline__ void wait_lds() {
   if constexpr (N == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -292,11 +296,29 @@ __device__ __forceinline__ void wait_lds() {
   else if constexpr (N == 12) asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
   else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
+// wait until at most n (runtime: 0, g or 2g for g DMA instructions per tile) are outstanding
+template <int G>
+__device__ __forceinline__ void wait_dma(int tiles) {
+  if (tiles <= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if (tiles == 1) {
+    if constexpr (G == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    if constexpr (G == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+  }
+}
 
-template <bool AT, bool BT, int EPI>
+// BK: k-tile depth; DEPTH LDS stages, the copy of tile it + DEPTH - 1 issued while tile it is
+// multiplied. DEPTH 2 waits for the next tile's copy at every barrier (vmcnt(0)); deeper
+// pipelines keep DEPTH - 2 copies in flight across the barrier, which therefore is a raw
+// s_barrier (__syncthreads() would wait for every outstanding LDS-DMA).
+template <bool AT, bool BT, int EPI, int BK, int DEPTH>
 __global__ __launch_bounds__(WNT, 1) void gemm_bf16w_kernel(PParams pp) {
+  constexpr int IMG = WT * BK;  // bf16 elements per operand image
   const Params& p = pp.g;
-  __shared__ __attribute__((aligned(16))) short smem[4 * WIMG];  // [stage][A | B]
+  __shared__ __attribute__((aligned(16))) short smem[DEPTH * 2 * IMG];  // [stage][A | B]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -305,8 +327,8 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16w_kernel(PParams pp) {
   const unsigned short* __restrict__ A = pp.A + t.bi * p.sA;
   const unsigned short* __restrict__ Bm = pp.B + t.bi * p.sB;
 
-  WLoad<!AT> la;
-  WLoad<BT> lb;
+  WLoad<!AT, BK> la;
+  WLoad<BT, BK> lb;
   la.init(p.lda, t.m0, p.M, wave, lane);
   lb.init(p.ldb, t.n0, p.N, wave, lane);
 
@@ -319,28 +341,39 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16w_kernel(PParams pp) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int npairs = (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
-  const int nkt = t.ks < t.ke ? (t.ke - t.ks + WBK - 1) / WBK : 0;
+  const int nkt = t.ks < t.ke ? (t.ke - t.ks + BK - 1) / BK : 0;
   const int total = npairs * nkt;
   int ipr = 0, ikt = 0;  // (pair, k-tile) of the next copy
   auto issue = [&](int stage) {
-    short* img = smem + stage * 2 * WIMG;
-    const int k0 = t.ks + ikt * WBK;
+    short* img = smem + stage * 2 * IMG;
+    const int k0 = t.ks + ikt * BK;
     const int pab = pp.pab >> (4 * ipr);
     la.issue(A + (pab & 3) * pp.pA, p.lda, k0, t.ke, img, wave);
-    lb.issue(Bm + ((pab >> 2) & 3) * pp.pB, p.ldb, k0, t.ke, img + WIMG, wave);
+    lb.issue(Bm + ((pab >> 2) & 3) * pp.pB, p.ldb, k0, t.ke, img + IMG, wave);
     if (++ikt == nkt) { ikt = 0; ++ipr; }
   };
-  constexpr int NRD = 4 * WLoad<!AT>::NRD + 2 * WLoad<BT>::NRD;  // LDS reads per k16-step
+  constexpr int NRD = 4 * WLoad<!AT, BK>::NRD + 2 * WLoad<BT, BK>::NRD;  // LDS reads / k16-step
+  constexpr int G = 2 * (BK / 16);  // DMA instructions per thread per tile
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
-  if (total > 0) issue(0);
+#pragma unroll
+  for (int s = 0; s < DEPTH - 1; ++s)
+    if (s < total) issue(s);
   for (int it = 0; it < total; ++it) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // stage it&1 landed for all waves; stage (it+1)&1 no longer read
-    if (it + 1 < total) issue((it + 1) & 1);
-    const short* sa = smem + (it & 1) * 2 * WIMG;
-    const short* sb = sa + WIMG;
-    const unsigned la0 = lds0 + 2u * (unsigned)((it & 1) * 2 * WIMG);
-    const unsigned lb0 = la0 + 2u * WIMG;
+    const int stage = it % DEPTH;
+    if constexpr (DEPTH == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();  // tile it landed for all waves; the other stage is no longer read
+    } else {
+      const int issued = min(total, it + DEPTH - 1);
+      wait_dma<G>(issued - it - 1);  // this wave's copies of tile it have landed
+      __builtin_amdgcn_s_barrier();  // ... for every wave; stage (it-1) % DEPTH no longer read
+      asm volatile("" ::: "memory");
+    }
+    if (it + DEPTH - 1 < total) issue((it + DEPTH - 1) % DEPTH);
+    const short* sa = smem + stage * 2 * IMG;
+    const short* sb = sa + IMG;
+    const unsigned la0 = lds0 + 2u * (unsigned)(stage * 2 * IMG);
+    const unsigned lb0 = la0 + 2u * IMG;
     bf16x8 fa[2][4], fb[2][2];
     auto rd = [&](int ks, bf16x8 (&a)[4], bf16x8 (&b)[2]) {
 #pragma unroll
@@ -350,8 +383,8 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16w_kernel(PParams pp) {
     };
     rd(0, fa[0], fb[0]);
 #pragma unroll
-    for (int ks = 0; ks < WBK / 16; ++ks) {
-      if (ks + 1 < WBK / 16) {
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      if (ks + 1 < BK / 16) {
         rd(ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
         wait_lds<NRD>();
       } else {
@@ -367,23 +400,33 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16w_kernel(PParams pp) {
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
 }
 
-template <bool AT, bool BT, int EPI>
+template <bool AT, bool BT, int EPI, int BK, int DEPTH>
 hipError_t launch_w(const PParams& p, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
-  hipLaunchKernelGGL((gemm_bf16w_kernel<AT, BT, EPI>), dim3(nwg), dim3(WNT), 0, st, p);
+  hipLaunchKernelGGL((gemm_bf16w_kernel<AT, BT, EPI, BK, DEPTH>), dim3(nwg), dim3(WNT), 0, st, p);
   return hipGetLastError();
 }
 
+template <int EPI, int BK, int DEPTH>
+hipError_t launch_wide_t(const PParams& p, bool at, bool bt, hipStream_t st) {
+  if (!at && !bt) return launch_w<false, false, EPI, BK, DEPTH>(p, st);
+  if (at && !bt) return launch_w<true, false, EPI, BK, DEPTH>(p, st);
+  if (!at && bt) return launch_w<false, true, EPI, BK, DEPTH>(p, st);
+  return launch_w<true, true, EPI, BK, DEPTH>(p, st);
+}
+
+// wide variants (diagnostics): 5 = BK 32 x 4 stages; otherwise BK 64 x 2 stages
 template <int EPI>
-hipError_t launch_wide(const PParams& p, bool at, bool bt, hipStream_t st) {
-  if (!at && !bt) return launch_w<false, false, EPI>(p, st);
-  if (at && !bt) return launch_w<true, false, EPI>(p, st);
-  if (!at && bt) return launch_w<false, true, EPI>(p, st);
-  return launch_w<true, true, EPI>(p, st);
+hipError_t launch_wide(const PParams& p, bool at, bool bt, int variant, hipStream_t st) {
+  if constexpr (EPI == EPI_STORE) {
+    if (variant == 5) return launch_wide_t<EPI, 32, 4>(p, at, bt, st);
+  }
+  return launch_wide_t<EPI, 64, 2>(p, at, bt, st);
 }
 
 template <bool AT, bool BT, int EPI, int BK, bool DB>
@@ -419,7 +462,7 @@ hipError_t launch_var(const PParams& p, bool at, bool bt, int variant, hipStream
 bool gemm_bf16_wide(const GemmDesc& d) {
   if (d.prec == GEMM_F32) return false;
   if (d.variant == 1 || d.variant == 2 || d.variant == 4) return false;  // 128x128 variants
-  if (d.variant != 3 && (d.M < 256 || d.N < 256)) return false;
+  if (d.variant != 3 && d.variant != 5 && (d.M < 256 || d.N < 256)) return false;
   auto a8 = [](long long v) { return (v & 7) == 0; };
   if (!a8(d.lda) || !a8(d.ldb) || !a8(d.pA) || !a8(d.pB)) return false;
   if (d.batch > 1 && (!a8(d.sA) || !a8(d.sB))) return false;
@@ -430,15 +473,15 @@ bool gemm_bf16_wide(const GemmDesc& d) {
 int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws) {
   if (d.epi.mode == EPI_BCE || d.epi.mode == EPI_SIGMOID) return 1;
   const long long tiles = (long long)((d.M + WT - 1) / WT) * ((d.N + WT - 1) / WT) * d.batch;
-  const int kt = (d.K + WBK - 1) / WBK;
+  const int kt = (d.K + 63) / 64;
   const int T = d.nA > d.nB ? d.nA : d.nB;
   int np = 0;
   for (int i = 0; i < d.nA; ++i)
     for (int j = 0; j < d.nB; ++j) np += i + j < T;
   if (d.dynA) np = (np + (d.nB < T ? d.nB : T)) / 2;  // A's residual planes often all zero
-  // one 256x256x64 k-tile per CU ~1.07 us (MFMA-bound, 2 waves/SIMD); + prologue/epilogue;
+  // one 256x256x64 k-tile per CU (one workgroup per CU); + prologue/epilogue;
   // split-K adds the fp32 slab round trip and the reduction launch
-  const double t_kt = 1.07e-6;
+  const double t_kt = 1.9e-6;  // measured: 4096^3 at 1.06 PF/s = 1.94 us per k-tile per CU
   double best = 1e30;
   int best_s = 1;
   for (int s = 1; s <= 32; ++s) {
@@ -473,11 +516,11 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
     p.g.ntm = (d.M + WT - 1) / WT;
     p.g.ntn = (d.N + WT - 1) / WT;
     switch (epi) {
-      case EPI_STORE: return launch_wide<EPI_STORE>(p, d.at, d.bt, st);
-      case EPI_ACT: return launch_wide<EPI_ACT>(p, d.at, d.bt, st);
-      case EPI_DACT: return launch_wide<EPI_DACT>(p, d.at, d.bt, st);
-      case EPI_BCE: return launch_wide<EPI_BCE>(p, d.at, d.bt, st);
-      case EPI_SIGMOID: return launch_wide<EPI_SIGMOID>(p, d.at, d.bt, st);
+      case EPI_STORE: return launch_wide<EPI_STORE>(p, d.at, d.bt, d.variant, st);
+      case EPI_ACT: return launch_wide<EPI_ACT>(p, d.at, d.bt, d.variant, st);
+      case EPI_DACT: return launch_wide<EPI_DACT>(p, d.at, d.bt, d.variant, st);
+      case EPI_BCE: return launch_wide<EPI_BCE>(p, d.at, d.bt, d.variant, st);
+      case EPI_SIGMOID: return launch_wide<EPI_SIGMOID>(p, d.at, d.bt, d.variant, st);
       default: return hipErrorInvalidValue;
     }
   }

@@ -32,6 +32,11 @@ __device__ __forceinline__ float dact_f(float g, float y, int act) {
   return y < 0.f ? g * (y + 1.f) : g;              // TF EluGrad (on the output)
 }
 __device__ __forceinline__ float sigmoid_f(float v) { return 1.f / (1.f + expf(-v)); }
+// hardware transcendentals (v_exp_f32 / v_log_f32 / v_rcp_f32, ~1e-7 relative): the BCE
+// epilogue evaluates them for every decoder output element (D x B per step)
+__device__ __forceinline__ float sigmoid_fast(float v) {
+  return __builtin_amdgcn_rcpf(1.f + __expf(-v));
+}
 
 // bijective XCD remap: consecutive logical tiles land on the same XCD (blockIdx % 8 group)
 __device__ __forceinline__ int xcd_remap(int b, int nwg) {
@@ -89,39 +94,70 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
   const int lane = tid & 63;
   const int fr = lane & 31, fk = lane >> 5;
   float* __restrict__ C = p.C + (size_t)t.z * p.sC;  // z = bi*split + si (slab) or bi (split==1)
-  unsigned short* cp = p.epi.cp ? p.epi.cp + (size_t)t.z * p.sC : nullptr;
+  unsigned short* __restrict__ cp = p.epi.cp ? p.epi.cp + (size_t)t.z * p.sC : nullptr;
+  const GemmEpi& e = p.epi;
   const int rbase = t.m0 + wm * MI * 32 + 4 * fk;
   const int cbase = t.n0 + wn * NI * 32 + fr;
-  if constexpr (EPI == EPI_BCE) {
-    const GemmEpi& e = p.epi;
+  // Each 32-row block: the operand the epilogue reads (aux for DACT, the target x for BCE)
+  // is loaded for all 16 x NI elements first, then the outputs are computed and stored.
+  // (Interleaving load -> use -> store per element serialises one memory latency per element:
+  // the stores may alias the loads.)
+  constexpr bool READS = EPI == EPI_DACT || EPI == EPI_BCE;
+  const float* __restrict__ src = EPI == EPI_DACT ? e.aux : e.x;
+  const int lds_ = EPI == EPI_DACT ? e.ld_aux : e.ldx;
 #pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
+  for (int mi = 0; mi < MI; ++mi) {
+    float sv[16][NI];
+    if constexpr (READS) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = rbase + mi * 32 + (r & 3) + 8 * (r >> 2);
-        float rs = 0.f;
+        int sr = row < p.M ? row : p.M - 1;
+        if constexpr (EPI == EPI_DACT) sr = sr >= e.remap_split ? sr - e.remap_shift : sr;
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
-          const int col = cbase + ni * 32;
-          if (row < p.M && col < p.N) {
-            const float yv = sigmoid_f(acc[mi][ni][r]);
-            const float xv = e.x[(size_t)row * e.ldx + col];
+          int col = cbase + ni * 32;
+          col = col < p.N ? col : p.N - 1;
+          sv[r][ni] = src[(size_t)sr * lds_ + col];
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = rbase + mi * 32 + (r & 3) + 8 * (r >> 2);
+      float rs = 0.f;
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int col = cbase + ni * 32;
+        if (row < p.M && col < p.N) {
+          const size_t o = (size_t)row * p.ldc + col;
+          float v = acc[mi][ni][r];
+          if constexpr (EPI == EPI_BCE) {
+            const float yv = sigmoid_fast(v);
+            const float xv = sv[r][ni];
             // -log(y^x (1-y)^(1-x)) with TF pow(0,0) = 1 (no epsilon), 11a/vae.py:266-269
             float term = 0.f;
-            if (xv != 0.f) term += xv * logf(yv);
-            if (xv != 1.f) term += (1.f - xv) * logf(1.f - yv);
+            if (xv != 0.f) term += xv * __logf(yv);
+            if (xv != 1.f) term += (1.f - xv) * __logf(1.f - yv);
             rs += term;
-            const float du = (yv - xv) * e.scale;
-            C[(size_t)row * p.ldc + col] = du;
-            if (cp) store_planes(cp, e.pc, e.ncp, (size_t)row * p.ldc + col, du);
+            v = (yv - xv) * e.scale;
             if (e.y) e.y[(size_t)row * e.ldy + col] = yv;
           }
+          if constexpr (EPI == EPI_ACT) v = act_f(v, e.act);
+          if constexpr (EPI == EPI_SIGMOID) v = sigmoid_f(v);
+          if constexpr (EPI == EPI_DACT) v = dact_f(v, sv[r][ni], e.act);
+          C[o] = v;
+          if (cp) store_planes(cp, e.pc, e.ncp, o, v);
         }
+      }
+      if constexpr (EPI == EPI_BCE) {
 #pragma unroll
         for (int off = 16; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
         if (fr == 0) red[wn * TBM + (row - t.m0)] = rs;  // lanes 0 and 32
       }
     }
+  }
+  if constexpr (EPI == EPI_BCE) {
     __syncthreads();
     constexpr int WPB = 128 / (NI * 32);  // waves per 128-column block
     constexpr int NBT = NWN / WPB;        // 128-column blocks per tile
@@ -134,29 +170,6 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
 #pragma unroll
         for (int w = 0; w < WPB; ++w) s_ += red[(b * WPB + w) * TBM + r];
         e.rowpart[(size_t)(t.m0 + r) * nblk + gb] = -s_;
-      }
-    }
-  } else {
-#pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rbase + mi * 32 + (r & 3) + 8 * (r >> 2);
-        if (row >= p.M) continue;
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) {
-          const int col = cbase + ni * 32;
-          if (col >= p.N) continue;
-          float v = acc[mi][ni][r];
-          if constexpr (EPI == EPI_ACT) v = act_f(v, p.epi.act);
-          if constexpr (EPI == EPI_SIGMOID) v = sigmoid_f(v);
-          if constexpr (EPI == EPI_DACT) {
-            const int ar = row >= p.epi.remap_split ? row - p.epi.remap_shift : row;
-            v = dact_f(v, p.epi.aux[(size_t)ar * p.epi.ld_aux + col], p.epi.act);
-          }
-          C[(size_t)row * p.ldc + col] = v;
-          if (cp) store_planes(cp, p.epi.pc, p.epi.ncp, (size_t)row * p.ldc + col, v);
-        }
       }
     }
   }

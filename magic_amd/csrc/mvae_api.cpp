@@ -67,6 +67,7 @@ struct mvae_ctx {
   std::vector<PlaneBuf> planes;
   int np = 0;            // planes per buffer: 0 (fp32 mode), 1 (bf16), 3 (f32x)
   int* dyn = nullptr;    // f32x: residual planes of the de-interleaved pixels nonzero?
+  int x32mask = 7;       // fp32 row blocks of xs the step reads (bit c: 0 rot, 1 lock, 2 key)
   // schedule (each GEMM tagged with its timing region)
   std::vector<GemmDesc> fwd_enc;  // encoder layers + head
   GemmDesc f_d1, f_d2, f_out;
@@ -461,12 +462,23 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     d.Bp = b.p; d.pB = b.stride; d.nB = c->np;
     d.epi.cp = o.p; d.epi.pc = o.stride; d.epi.ncp = o.p ? c->np : 0;
     d.dynA = (c->dyn && d.A >= c->xs && d.A < c->xs + (size_t)3 * B * c->ldx) ? c->dyn : nullptr;
+    // exact split: GEMMs the 256x256 bf16 kernel does not serve (a dimension < 256: the
+    // latent head, thin decoder layers) run faster as one native fp32 MFMA GEMM than as six
+    // bf16 plane products on the 128x128 kernel; same accuracy class
+    if (gp == GEMM_F32X && !gemm_bf16_wide(d)) d.prec = GEMM_F32;
   };
   for (auto* v : {&c->fwd_enc, &c->bwd_dec, &c->bwd_enc})
     for (auto& d : *v) wire(d);
   wire(c->f_d1);
   wire(c->f_d2);
   wire(c->f_out);
+  // fp32 xs rows: the BCE target (lock block) always; everything when a GEMM reads xs in fp32
+  if (c->np) {
+    c->x32mask = 2;
+    for (auto* v : {&c->fwd_enc, &c->bwd_enc})
+      for (auto& d : *v)
+        if (d.prec == GEMM_F32 && d.A >= c->xs && d.A < c->xs + (size_t)3 * B * c->ldx) c->x32mask = 7;
+  }
   for (auto* v : {&c->fwd_enc, &c->bwd_dec, &c->bwd_enc})
     for (auto& d : *v)
       if (c->np && (!d.Ap || !d.Bp)) {
@@ -566,6 +578,9 @@ int mvae_buffer(mvae_ctx* ctx, int which, float** ptr, size_t* count) {
     case MVAE_BUF_GRADS_DEC: *ptr = ctx->grads + ctx->n_enc; *count = ctx->n_all - ctx->n_enc; break;
     case MVAE_BUF_DEAD: *ptr = ctx->dead; *count = (size_t)ctx->d1 * ctx->D + ctx->D; break;
     case MVAE_BUF_EPS: *ptr = ctx->eps; *count = (size_t)3 * ctx->B * ctx->L; break;
+    case MVAE_BUF_DYN:
+      if (!ctx->dyn) return fail(ctx, MVAE_EINVAL, "no dyn flag in this precision mode");
+      *ptr = reinterpret_cast<float*>(ctx->dyn); *count = 1; break;
     default: return fail(ctx, MVAE_EINVAL, "bad buffer id");
   }
   return MVAE_OK;
@@ -609,7 +624,8 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
   {
     TIMED("deinterleave");
     if (c->dyn) MV_CHECK(hipMemsetAsync(c->dyn, 0, sizeof(int), st));
-    MV_CHECK(launch_deinterleave(x, c->xs, planes_of(c, c->xs), c->dyn, c->B, c->D, c->ldx, st));
+    MV_CHECK(launch_deinterleave(x, c->xs, planes_of(c, c->xs), c->dyn, c->B, c->D, c->ldx,
+                                 c->x32mask, st));
   }
   const size_t ne = (size_t)3 * c->B * c->L;
   {
@@ -921,7 +937,7 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   GemmDesc d = gd(M, N, K, nullptr, lda, at != 0, nullptr, ldb, bt != 0, nullptr, N);
   d.batch = batch; d.sA = (long long)sa; d.sB = (long long)sb; d.sC = (long long)M * N;
   d.variant = variant & 15;
-  d.prec = variant >> 4;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
+  d.prec = (variant >> 4) & 15;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
   unsigned short* planes = nullptr;
   const int np = d.prec == GEMM_F32 ? 0 : (d.prec == GEMM_BF16 ? 1 : 3);
   hipError_t e = hipMalloc(&A, na * 4);
@@ -938,6 +954,27 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
     d.Ap = A_.p; d.pA = A_.stride; d.nA = np;
     d.Bp = B_.p; d.pB = B_.stride; d.nB = np;
   }
+  // epilogue (variant >> 8): the step's fused epilogues with their operand reads and the
+  // output planes the next GEMM would read
+  const int epi = (variant >> 8) & 15;
+  float *aux = nullptr, *rowpart = nullptr;
+  unsigned short* cpl = nullptr;
+  if (e == hipSuccess && epi != EPI_STORE) {
+    if (epi > EPI_SIGMOID) e = hipErrorInvalidValue;
+    d.epi.mode = epi;
+    d.epi.act = ACT_TANH;
+    if (e == hipSuccess) e = hipMalloc(&aux, (size_t)M * N * 4);
+    if (e == hipSuccess) e = launch_normal(aux, (size_t)M * N, 3, 0, st);
+    if (e == hipSuccess && epi == EPI_BCE) e = hipMalloc(&rowpart, (size_t)M * gemm_bce_nblk(N) * 4);
+    d.epi.aux = aux; d.epi.ld_aux = N;
+    d.epi.x = aux; d.epi.ldx = N;
+    d.epi.rowpart = rowpart;
+    d.epi.scale = 1.f / M;
+    if (e == hipSuccess && np) {
+      e = hipMalloc(&cpl, (size_t)np * nc * 2);
+      d.epi.cp = cpl; d.epi.pc = (long long)nc; d.epi.ncp = np;
+    }
+  }
   const size_t ws_n = gemm_workspace_elems(d);
   if (e == hipSuccess && ws_n) e = hipMalloc(&ws, ws_n * 4);
   hipEvent_t t0 = nullptr, t1 = nullptr;
@@ -953,8 +990,9 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   *avg_ms = ms / iters;
   if (t0) (void)hipEventDestroy(t0);
   if (t1) (void)hipEventDestroy(t1);
-  for (float* p : {A, Bm, Cm, ws}) if (p) (void)hipFree(p);
+  for (float* p : {A, Bm, Cm, ws, aux, rowpart}) if (p) (void)hipFree(p);
   if (planes) (void)hipFree(planes);
+  if (cpl) (void)hipFree(cpl);
   if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
   return MVAE_OK;
 }

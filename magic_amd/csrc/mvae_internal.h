@@ -80,8 +80,10 @@ struct Planes {
   long long stride = 0;
   int n = 0;
 };
+// f32mask: bit c -> write fp32 rows of block c (0 rot, 1 lock, 2 key). Plane 0 always (when
+// xp.p); with 3 planes, planes 1-2 are written only when *dyn ends up nonzero.
 hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int B, int D,
-                               int ldx, hipStream_t st);
+                               int ldx, int f32mask, hipStream_t st);
 hipError_t launch_normal(float* out, size_t n, uint64_t seed, uint64_t counter, hipStream_t st);
 hipError_t launch_latent_fwd(const float* ms, const float* eps, float* z, const Planes& zp, int B,
                              int L, int ldz, hipStream_t st);

@@ -35,40 +35,56 @@ __device__ __forceinline__ int eps_slot(int blk) { return blk == 0 ? 1 : (blk ==
 // x[b][p*3 + c] (c: 0 lock, 1 rotated lock, 2 key; 11a/overlap_input.py:117-119,201)
 //  -> xs[(blk*B + b)][p], blk = {rot:0, lock:1, key:2}. Each thread moves 4 pixels:
 // three 16-B loads, three 16-B stores (coalesced both ways).
+// bf16 bits of v rounded to nearest even, and the exact remainder v - bf16(v)
+__device__ __forceinline__ unsigned short bf16_rn(float v, float& rem) {
+  const unsigned short b = __builtin_bit_cast(unsigned short, __float2bfloat16(v));
+  rem = v - __uint_as_float((unsigned)b << 16);
+  return b;
+}
+__device__ __forceinline__ uint2 pack4(unsigned short a, unsigned short b, unsigned short c,
+                                       unsigned short d) {
+  return make_uint2((unsigned)a | (unsigned)b << 16, (unsigned)c | (unsigned)d << 16);
+}
+
+// [B, D, 3] interleaved (lock, rotated, key) -> row blocks [rot | lock | key] of the layer-0
+// operand: fp32 rows for the blocks in f32mask (bit c: block c; plane modes keep only the lock
+// block, the BCE target) and the RN bf16 plane 0 (8-byte stores). In the exact-split mode the
+// residual planes are NOT written here: the kernel only raises *dyn when some pixel is not
+// exact in bf16, and residual_planes_kernel then writes planes 1 and 2 (binary shape images
+// never pay for them; the GEMMs read the residual planes only when *dyn != 0).
 __global__ void deinterleave_vec_kernel(const float4* __restrict__ x, float* __restrict__ xs,
-                                        unsigned short* __restrict__ xp, long long ps, int np,
-                                        int* __restrict__ dyn, int B, int D, int ldx) {
+                                        unsigned short* __restrict__ xp, int* __restrict__ dyn,
+                                        int B, int D, int ldx, int f32mask) {
   const int b = blockIdx.y;
   const int q = blockIdx.x * blockDim.x + threadIdx.x;  // pixel quad
-  if (q * 4 >= D) return;
-  const float4* src = x + ((size_t)b * 3 * D) / 4 + 3 * q;
-  const float4 v0 = src[0], v1 = src[1], v2 = src[2];
-  // pixels p0..p3: (l,r,k) = (v0.x v0.y v0.z) (v0.w v1.x v1.y) (v1.z v1.w v2.x) (v2.y v2.z v2.w)
-  const float4 lock = make_float4(v0.x, v0.w, v1.z, v2.y);
-  const float4 rot = make_float4(v0.y, v1.x, v1.w, v2.z);
-  const float4 key = make_float4(v0.z, v1.y, v2.x, v2.w);
-  const size_t col = 4 * (size_t)q;
-  *reinterpret_cast<float4*>(xs + (size_t)b * ldx + col) = rot;
-  *reinterpret_cast<float4*>(xs + (size_t)(B + b) * ldx + col) = lock;
-  *reinterpret_cast<float4*>(xs + (size_t)(2 * B + b) * ldx + col) = key;
-  if (xp) {
-    const float4 vv[3] = {rot, lock, key};
-    bool nz = false;
+  bool nz = false;
+  if (q * 4 < D) {
+    const float4* src = x + ((size_t)b * 3 * D) / 4 + 3 * q;
+    const float4 v0 = src[0], v1 = src[1], v2 = src[2];
+    // pixels p0..p3: (l,r,k) = (v0.x v0.y v0.z) (v0.w v1.x v1.y) (v1.z v1.w v2.x) (v2.y v2.z v2.w)
+    const float4 vv[3] = {make_float4(v0.y, v1.x, v1.w, v2.z),   // rot
+                          make_float4(v0.x, v0.w, v1.z, v2.y),   // lock
+                          make_float4(v0.z, v1.y, v2.x, v2.w)};  // key
+    const size_t col = 4 * (size_t)q;
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const size_t o = (size_t)(c * B + b) * ldx + col;
-      nz |= planes_put(xp, ps, np, o + 0, vv[c].x);
-      nz |= planes_put(xp, ps, np, o + 1, vv[c].y);
-      nz |= planes_put(xp, ps, np, o + 2, vv[c].z);
-      nz |= planes_put(xp, ps, np, o + 3, vv[c].w);
+      if (f32mask >> c & 1) *reinterpret_cast<float4*>(xs + o) = vv[c];
+      if (xp) {
+        float r0, r1, r2, r3;
+        const uint2 w = pack4(bf16_rn(vv[c].x, r0), bf16_rn(vv[c].y, r1), bf16_rn(vv[c].z, r2),
+                              bf16_rn(vv[c].w, r3));
+        *reinterpret_cast<uint2*>(xp + o) = w;
+        nz |= (r0 != 0.f) | (r1 != 0.f) | (r2 != 0.f) | (r3 != 0.f);
+      }
     }
-    if (dyn && __ballot(nz) != 0 && (threadIdx.x & 63) == 0) atomicOr(dyn, 1);
   }
+  if (dyn && __ballot(nz) != 0 && (threadIdx.x & 63) == 0) atomicOr(dyn, 1);
 }
 
 __global__ void deinterleave_scalar_kernel(const float* __restrict__ x, float* __restrict__ xs,
-                                           unsigned short* __restrict__ xp, long long ps, int np,
-                                           int* __restrict__ dyn, int B, int D, int ldx) {
+                                           unsigned short* __restrict__ xp, int* __restrict__ dyn,
+                                           int B, int D, int ldx, int f32mask) {
   const int b = blockIdx.y;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   bool nz = false;
@@ -77,11 +93,38 @@ __global__ void deinterleave_scalar_kernel(const float* __restrict__ x, float* _
     const float v[3] = {src[1], src[0], src[2]};  // rot, lock, key
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      xs[(size_t)(c * B + b) * ldx + p] = v[c];
-      if (xp) nz |= planes_put(xp, ps, np, (size_t)(c * B + b) * ldx + p, v[c]);
+      const size_t o = (size_t)(c * B + b) * ldx + p;
+      if (f32mask >> c & 1) xs[o] = v[c];
+      if (xp) {
+        float r;
+        xp[o] = bf16_rn(v[c], r);
+        nz |= r != 0.f;
+      }
     }
   }
   if (dyn && __ballot(nz) != 0 && (threadIdx.x & 63) == 0) atomicOr(dyn, 1);
+}
+
+// planes 1 and 2 of the exact split of the layer-0 operand, only when *dyn != 0
+__global__ void residual_planes_kernel(const float* __restrict__ x, unsigned short* __restrict__ xp,
+                                       long long ps, const int* __restrict__ dyn, int B, int D,
+                                       int ldx) {
+  if (*dyn == 0) return;
+  const size_t n = (size_t)B * D;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = i / D, p = i - b * D;
+    const float* src = x + b * 3 * D + 3 * p;
+    const float v[3] = {src[1], src[0], src[2]};  // rot, lock, key
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      const size_t o = (size_t)(c * B + b) * ldx + p;
+      float r1, r2, r3;
+      (void)bf16_rn(v[c], r1);
+      xp[ps + o] = bf16_rn(r1, r2);
+      xp[2 * ps + o] = bf16_rn(r2, r3);
+    }
+  }
 }
 
 // ---------------------------------------------------------------- N(0,1) sampler
@@ -406,16 +449,19 @@ inline unsigned nblocks(size_t n, int bs) { return (unsigned)((n + bs - 1) / bs)
 }  // namespace
 
 hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int B, int D,
-                               int ldx, hipStream_t st) {
+                               int ldx, int f32mask, hipStream_t st) {
   if ((D % 4) == 0 && (reinterpret_cast<uintptr_t>(x) % 16) == 0 && (ldx % 4) == 0) {
     dim3 g(nblocks(D / 4, 256), B);
     hipLaunchKernelGGL(deinterleave_vec_kernel, g, dim3(256), 0, st,
-                       reinterpret_cast<const float4*>(x), xs, xp.p, xp.stride, xp.n, dyn, B, D, ldx);
+                       reinterpret_cast<const float4*>(x), xs, xp.p, dyn, B, D, ldx, f32mask);
   } else {
     dim3 g(nblocks(D, 256), B);
-    hipLaunchKernelGGL(deinterleave_scalar_kernel, g, dim3(256), 0, st, x, xs, xp.p, xp.stride, xp.n,
-                       dyn, B, D, ldx);
+    hipLaunchKernelGGL(deinterleave_scalar_kernel, g, dim3(256), 0, st, x, xs, xp.p, dyn, B, D, ldx,
+                       f32mask);
   }
+  if (xp.n == 3 && dyn)
+    hipLaunchKernelGGL(residual_planes_kernel, dim3(2048), dim3(256), 0, st, x, xp.p, xp.stride, dyn,
+                       B, D, ldx);
   return hipGetLastError();
 }
 

@@ -21,17 +21,19 @@ from magic_amd.config import baseline_config  # noqa: E402
 def shapes(cfg):
     B, D, e, L = cfg.batch, cfg.D, cfg.enc[0], cfg.latent
     d1 = cfg.dec[1]
+    # (name, M, N, K, at, bt, batch, epilogue: 0 store, 1 act, 2 dact, 3 bce)
     return [
-        ("enc_fwd_0", 3 * B, e, D + 1, 0, 0, 1),
-        ("enc_bwd_w_0", D + 1, e, 2 * B, 1, 0, 2),
-        ("dec_fwd_out", B, D, d1 + 1, 0, 0, 1),
-        ("dec_bwd_d_out", B, d1, D, 0, 1, 1),
-        ("dec_bwd_w_out", d1 + 1, D, B, 1, 0, 1),
-        ("enc_fwd_h", 3 * B, e, e + 1, 0, 0, 1),
-        ("enc_bwd_d_h", 4 * B, e, e, 0, 1, 1),
-        ("enc_bwd_w_h", e + 1, e, 2 * B, 1, 0, 2),
-        ("head_fwd", 3 * B, 2 * L, e + 1, 0, 0, 1),
-        ("square4096", 4096, 4096, 4096, 0, 0, 1),
+        ("enc_fwd_0", 3 * B, e, D + 1, 0, 0, 1, 1),
+        ("enc_bwd_w_0", D + 1, e, 2 * B, 1, 0, 2, 0),
+        ("dec_fwd_out", B, D, d1 + 1, 0, 0, 1, 3),
+        ("dec_bwd_d_out", B, d1, D, 0, 1, 1, 2),
+        ("dec_bwd_w_out", d1 + 1, D, B, 1, 0, 1, 0),
+        ("enc_fwd_h", 3 * B, e, e + 1, 0, 0, 1, 1),
+        ("enc_bwd_d_h", 4 * B, e, e, 0, 1, 1, 2),
+        ("enc_bwd_w_h", e + 1, e, 2 * B, 1, 0, 2, 0),
+        ("head_fwd", 3 * B, 2 * L, e + 1, 0, 0, 1, 0),
+        ("head_bwd_d", 4 * B, e, 2 * L, 0, 1, 1, 2),
+        ("square4096", 4096, 4096, 4096, 0, 0, 1, 0),
     ]
 
 
@@ -41,6 +43,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--config", default="C2")
+    ap.add_argument("--epilogues", action="store_true", help="run each shape with its step epilogue")
     args = ap.parse_args()
     lib = _lib.load()
     torch.cuda.init()
@@ -49,15 +52,16 @@ def main():
     variants = [int(v) for v in args.variants.split(",")]
     res = {}
     for _ in range(args.rounds):
-        for name, M, N, K, at, bt, batch in shapes(cfg):
+        for name, M, N, K, at, bt, batch, epi in shapes(cfg):
             for v in variants:
                 ms = C.c_float()
-                rc = lib.mvae_bench_gemm(M, N, K, at, bt, batch, v, args.iters, st, C.byref(ms))
+                vv = v | (epi << 8 if args.epilogues else 0)
+                rc = lib.mvae_bench_gemm(M, N, K, at, bt, batch, vv, args.iters, st, C.byref(ms))
                 if rc != 0:
                     raise RuntimeError(lib.mvae_last_error(None))
                 res.setdefault((name, v), []).append(ms.value)
     print(f"{'shape':16s} {'MxNxK':>22s} batch " + " ".join(f"{'v' + str(v) + ' TF/s':>10s}" for v in variants))
-    for name, M, N, K, at, bt, batch in shapes(cfg):
+    for name, M, N, K, at, bt, batch, epi in shapes(cfg):
         fl = 2.0 * M * N * K * batch
         cells = []
         for v in variants:
