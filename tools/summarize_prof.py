@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Summarise a rocprofv3 --kernel-trace CSV: per (kernel, grid) dispatch group, the call
 count and mean/min/max duration, so templated GEMM launches of different shapes are
-distinguishable. Usage: summarize_prof.py <run_kernel_trace.csv> [--top N]"""
+distinguishable (rocprofv3 demangles without template arguments, so instantiations are told
+apart by Kernel_Id). Usage: summarize_prof.py <run_kernel_trace.csv> [--top N]"""
 import collections
 import csv
 import sys
@@ -13,7 +14,7 @@ def main():
     rows = list(csv.DictReader(open(path)))
     g = collections.defaultdict(list)
     for r in rows:
-        name = r["Kernel_Name"]
+        name = f'{r["Kernel_Name"]} #{r.get("Kernel_Id", "")}'
         grid = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
         g[(name, grid)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     tot = sum(sum(v) for v in g.values())
