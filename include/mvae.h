@@ -96,8 +96,9 @@ enum {
   MVAE_BUF_DEAD = 8,     /* the never-trained decoder log-sigma variables               */
   MVAE_BUF_EPS = 9,      /* float[3,B,L]: eps of the last forward (given or generated)  */
   MVAE_BUF_DYN = 10      /* int32[1] (count 1): nonzero when the last batch's pixels are
-                            not all exact in bf16 (f32x mode: the layer-0 GEMMs then run
-                            all 6 plane pairs instead of 3); 0 in other modes             */
+                            not all exact in bf16 (f32x: the layer-0 GEMMs then run all 6
+                            plane pairs instead of 3; bf16/f32x: the BCE target is read in
+                            fp32 instead of bf16); absent in f32 mode                      */
 };
 
 int mvae_abi_version(void);

@@ -130,6 +130,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16p_kernel(PParams pp) {
   constexpr int STAGE = Geo<BK>::STAGE;
   constexpr int NB = DB ? 2 : 1;
   const Params& p = pp.g;
+  if (epi_skip<EPI>(p.epi)) return;
   __shared__ __attribute__((aligned(16))) short smem[2 * NB * STAGE];
   // image b of A at smem + b*STAGE, of B at smem + (NB+b)*STAGE
 
@@ -318,6 +319,7 @@ template <bool AT, bool BT, int EPI, int BK, int DEPTH>
 __global__ __launch_bounds__(WNT, 1) void gemm_bf16w_kernel(PParams pp) {
   constexpr int IMG = WT * BK;  // bf16 elements per operand image
   const Params& p = pp.g;
+  if (epi_skip<EPI>(p.epi)) return;
   __shared__ __attribute__((aligned(16))) short smem[DEPTH * 2 * IMG];  // [stage][A | B]
 
   const int tid = threadIdx.x;
@@ -402,6 +404,8 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16w_kernel(PParams pp) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  // C/D-layout epilogue: one 128-B row segment per half-wave store. (An LDS-transposed form
+  // with 16-B row stores measured slower on every step shape and spills with BCE.)
   epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
 }
 
@@ -471,7 +475,7 @@ bool gemm_bf16_wide(const GemmDesc& d) {
 }
 
 int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws) {
-  if (d.epi.mode == EPI_BCE || d.epi.mode == EPI_SIGMOID) return 1;
+  if (d.epi.mode == EPI_BCE || d.epi.mode == EPI_BCEB || d.epi.mode == EPI_SIGMOID) return 1;
   const long long tiles = (long long)((d.M + WT - 1) / WT) * ((d.N + WT - 1) / WT) * d.batch;
   const int kt = (d.K + 63) / 64;
   const int T = d.nA > d.nB ? d.nA : d.nB;
@@ -520,6 +524,7 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
       case EPI_ACT: return launch_wide<EPI_ACT>(p, d.at, d.bt, d.variant, st);
       case EPI_DACT: return launch_wide<EPI_DACT>(p, d.at, d.bt, d.variant, st);
       case EPI_BCE: return launch_wide<EPI_BCE>(p, d.at, d.bt, d.variant, st);
+      case EPI_BCEB: return launch_wide<EPI_BCEB>(p, d.at, d.bt, d.variant, st);
       case EPI_SIGMOID: return launch_wide<EPI_SIGMOID>(p, d.at, d.bt, d.variant, st);
       default: return hipErrorInvalidValue;
     }
@@ -529,6 +534,7 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
     case EPI_ACT: return launch_var<EPI_ACT>(p, d.at, d.bt, d.variant, st);
     case EPI_DACT: return launch_var<EPI_DACT>(p, d.at, d.bt, d.variant, st);
     case EPI_BCE: return launch_var<EPI_BCE>(p, d.at, d.bt, d.variant, st);
+    case EPI_BCEB: return launch_var<EPI_BCEB>(p, d.at, d.bt, d.variant, st);
     case EPI_SIGMOID: return launch_var<EPI_SIGMOID>(p, d.at, d.bt, d.variant, st);
     default: return hipErrorInvalidValue;
   }

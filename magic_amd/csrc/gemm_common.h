@@ -44,6 +44,28 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
+__device__ __forceinline__ float bf16_bits_to_f32(unsigned short b) {
+  return __uint_as_float((unsigned)b << 16);
+}
+// BCE epilogues: EPI_BCE reads the fp32 target, EPI_BCEB its bf16 plane (exact while *xdyn == 0,
+// i.e. every pixel of the batch is a bf16 value). With xdyn set both are launched and the one
+// that does not match *xdyn returns at once (uniform branch at kernel entry).
+template <int EPI>
+__device__ __forceinline__ bool epi_skip(const GemmEpi& e) {
+  if constexpr (EPI == EPI_BCE || EPI == EPI_BCEB)
+    return e.xdyn != nullptr && ((*e.xdyn == 0) != (EPI == EPI_BCEB));
+  return false;
+}
+// -log-likelihood term of one pixel, TF semantics log(y^x (1-y)^(1-x)) with pow(0,0) = 1 and
+// no epsilon (11a/vae.py:266-269). (A single-log form for binary targets makes hipcc spill
+// the wide kernel's accumulators across its main loop.)
+__device__ __forceinline__ float bce_term(float yv, float xv) {
+  float term = 0.f;
+  if (xv != 0.f) term += xv * __logf(yv);
+  if (xv != 1.f) term += (1.f - xv) * __logf(1.f - yv);
+  return term;
+}
+
 // v -> n bf16 planes (n = 1: round to nearest; n = 3: exact split, each residual exact)
 __device__ __forceinline__ void store_planes(unsigned short* cp, long long pc, int n, size_t idx,
                                              float v) {
@@ -102,7 +124,8 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
   // is loaded for all 16 x NI elements first, then the outputs are computed and stored.
   // (Interleaving load -> use -> store per element serialises one memory latency per element:
   // the stores may alias the loads.)
-  constexpr bool READS = EPI == EPI_DACT || EPI == EPI_BCE;
+  constexpr bool BCE = EPI == EPI_BCE || EPI == EPI_BCEB;
+  constexpr bool READS = EPI == EPI_DACT || BCE;
   const float* __restrict__ src = EPI == EPI_DACT ? e.aux : e.x;
   const int lds_ = EPI == EPI_DACT ? e.ld_aux : e.ldx;
 #pragma unroll
@@ -118,7 +141,8 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
         for (int ni = 0; ni < NI; ++ni) {
           int col = cbase + ni * 32;
           col = col < p.N ? col : p.N - 1;
-          sv[r][ni] = src[(size_t)sr * lds_ + col];
+          if constexpr (EPI == EPI_BCEB) sv[r][ni] = bf16_bits_to_f32(e.xp[(size_t)sr * lds_ + col]);
+          else sv[r][ni] = src[(size_t)sr * lds_ + col];
         }
       }
     }
@@ -132,32 +156,29 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
         if (row < p.M && col < p.N) {
           const size_t o = (size_t)row * p.ldc + col;
           float v = acc[mi][ni][r];
-          if constexpr (EPI == EPI_BCE) {
+          if constexpr (BCE) {
             const float yv = sigmoid_fast(v);
             const float xv = sv[r][ni];
             // -log(y^x (1-y)^(1-x)) with TF pow(0,0) = 1 (no epsilon), 11a/vae.py:266-269
-            float term = 0.f;
-            if (xv != 0.f) term += xv * __logf(yv);
-            if (xv != 1.f) term += (1.f - xv) * __logf(1.f - yv);
-            rs += term;
+            rs += bce_term(yv, xv);
             v = (yv - xv) * e.scale;
             if (e.y) e.y[(size_t)row * e.ldy + col] = yv;
           }
           if constexpr (EPI == EPI_ACT) v = act_f(v, e.act);
           if constexpr (EPI == EPI_SIGMOID) v = sigmoid_f(v);
           if constexpr (EPI == EPI_DACT) v = dact_f(v, sv[r][ni], e.act);
-          C[o] = v;
+          if (e.c32) C[o] = v;
           if (cp) store_planes(cp, e.pc, e.ncp, o, v);
         }
       }
-      if constexpr (EPI == EPI_BCE) {
+      if constexpr (BCE) {
 #pragma unroll
         for (int off = 16; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
         if (fr == 0) red[wn * TBM + (row - t.m0)] = rs;  // lanes 0 and 32
       }
     }
   }
-  if constexpr (EPI == EPI_BCE) {
+  if constexpr (BCE) {
     __syncthreads();
     constexpr int WPB = 128 / (NI * 32);  // waves per 128-column block
     constexpr int NBT = NWN / WPB;        // 128-column blocks per tile

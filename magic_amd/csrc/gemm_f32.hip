@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdint>
 
 namespace mvae {
 namespace {
@@ -120,6 +121,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(Params p) {
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
 
+  if (epi_skip<EPI>(p.epi)) return;
   const Tile t = tile_of(p, VAR != 2);
   const int bi = t.bi, m0 = t.m0, n0 = t.n0, ks = t.ks, ke = t.ke;
 
@@ -216,9 +218,76 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, in
       const int ar = row >= e.remap_split ? row - e.remap_shift : row;
       v = dact_f(v, e.aux[(size_t)ar * e.ld_aux + col], e.act);
     }
-    c[(size_t)row * ldc + col] = v;
+    if (e.c32) c[(size_t)row * ldc + col] = v;
     if (e.cp) store_planes(e.cp + bi * sC, e.pc, e.ncp, (size_t)row * ldc + col, v);
   }
+}
+
+// The same, 4 consecutive columns per thread: 16-B slab loads and fp32 stores, one 8-B store
+// per bf16 plane (the scalar form above is store-issue bound). Needs N, ldc, the plane and
+// batch strides multiples of 4 and 16-B aligned C / 8-B aligned planes (splitk_reduce4_ok).
+template <int EPI>
+__global__ void splitk_reduce4_kernel(const float* __restrict__ ws, int split, int M, int N,
+                                      float* __restrict__ C, int ldc, long long sC, GemmEpi e) {
+  const int bi = blockIdx.z;
+  const long long slab = (long long)M * N;
+  const float* w = ws + (size_t)bi * split * slab;
+  float* c = C + bi * sC;
+  unsigned short* cp = e.cp ? e.cp + bi * sC : nullptr;
+  const int n4 = N >> 2;
+  const long long total = (long long)M * n4;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int row = (int)(i / n4), col = 4 * (int)(i - (long long)row * n4);
+    const size_t si = (size_t)row * N + col;
+    float4 a = *reinterpret_cast<const float4*>(w + si);
+    for (int s = 1; s < split; ++s) {  // same order as the scalar kernel: ((s0 + s1) + s2) ...
+      const float4 u = *reinterpret_cast<const float4*>(w + s * slab + si);
+      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    }
+    float v[4] = {a.x, a.y, a.z, a.w};
+    if constexpr (EPI == EPI_ACT) {
+      if (e.act == ACT_TANH) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = act_f(v[j], ACT_TANH);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = act_f(v[j], ACT_ELU);
+      }
+    }
+    if constexpr (EPI == EPI_SIGMOID) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = sigmoid_f(v[j]);
+    }
+    if constexpr (EPI == EPI_DACT) {
+      const int ar = row >= e.remap_split ? row - e.remap_shift : row;
+      const float* x = e.aux + (size_t)ar * e.ld_aux + col;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = dact_f(v[j], x[j], e.act);
+    }
+    const size_t o = (size_t)row * ldc + col;
+    if (e.c32) *reinterpret_cast<float4*>(c + o) = make_float4(v[0], v[1], v[2], v[3]);
+    if (cp) {
+      float r[4] = {v[0], v[1], v[2], v[3]};
+      for (int t = 0; t < e.ncp; ++t) {
+        unsigned short b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          b[j] = __builtin_bit_cast(unsigned short, __float2bfloat16(r[j]));
+          r[j] -= bf16_bits_to_f32(b[j]);
+        }
+        *reinterpret_cast<uint2*>(cp + t * e.pc + o) =
+            make_uint2((unsigned)b[0] | (unsigned)b[1] << 16, (unsigned)b[2] | (unsigned)b[3] << 16);
+      }
+    }
+  }
+}
+
+bool splitk_reduce4_ok(const GemmDesc& d) {
+  auto a = [](const void* p, int n) { return (reinterpret_cast<uintptr_t>(p) & (n - 1)) == 0; };
+  if ((d.N & 3) || (d.ldc & 3) || (d.sC & 3) || !a(d.C, 16)) return false;
+  if (d.epi.cp && ((d.epi.pc & 3) || !a(d.epi.cp, 8))) return false;
+  return true;
 }
 
 template <bool AT, bool BT, int EPI, int VAR>
@@ -249,7 +318,7 @@ hipError_t launch_store(const Params& p, bool at, bool bt, int variant, hipStrea
 int gemm_bce_nblk(int N) { return (N + BN - 1) / BN; }
 
 int gemm_plan_split(const GemmDesc& d, size_t max_ws) {
-  if (d.epi.mode == EPI_BCE || d.epi.mode == EPI_SIGMOID) return 1;
+  if (d.epi.mode == EPI_BCE || d.epi.mode == EPI_BCEB || d.epi.mode == EPI_SIGMOID) return 1;
   if (gemm_bf16_wide(d)) return gemm_bf16_wide_split(d, max_ws);
   const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
   const long long tiles = (long long)ntm * ntn * d.batch;
@@ -287,6 +356,7 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   p.batch = d.batch;
   p.ntm = (d.M + BM - 1) / BM; p.ntn = (d.N + BN - 1) / BN;
   p.epi = d.epi;
+  if (d.prec == GEMM_F32) p.epi.xdyn = nullptr;  // fp32 kernels read the fp32 BCE target
   const int split = d.split > 0 ? d.split : gemm_plan_split(d, ws ? ws_elems : 0);
   p.split = split;
   const int kb = d.prec == GEMM_F32 ? BK : 64;  // k-tile of the kernel that runs
@@ -294,7 +364,16 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   p.kchunk = ((ktiles + split - 1) / split) * kb;
   if (split == 1) {
     p.C = d.C; p.ldc = d.ldc; p.sC = d.sC;
-    if (d.prec != GEMM_F32) return gemm_bf16_launch(p, d, d.epi.mode, st);
+    if (d.prec != GEMM_F32) {
+      // BCE with a bf16-plane target: two launches, each running only for its *xdyn state
+      if (d.epi.mode == EPI_BCE && d.epi.xp && d.epi.xdyn) {
+        hipError_t e = gemm_bf16_launch(p, d, EPI_BCE, st);
+        return e != hipSuccess ? e : gemm_bf16_launch(p, d, EPI_BCEB, st);
+      }
+      Params q = p;
+      q.epi.xdyn = nullptr;  // a single BCE launch always runs (fp32 target)
+      return gemm_bf16_launch(q, d, d.epi.mode, st);
+    }
     switch (d.epi.mode) {
       case EPI_STORE: return launch_store(p, d.at, d.bt, d.variant, st);
       case EPI_ACT: return launch_layout<EPI_ACT>(p, d.at, d.bt, st);
@@ -313,6 +392,25 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   const long long total = (long long)d.M * d.N;
   int grid = (int)std::min<long long>((total + 255) / 256, 2048);
   dim3 g(grid, 1, d.batch);
+  if (splitk_reduce4_ok(d)) {
+    dim3 g4((int)std::min<long long>((total / 4 + 255) / 256, 2048), 1, d.batch);
+    switch (d.epi.mode) {
+      case EPI_STORE:
+        hipLaunchKernelGGL(splitk_reduce4_kernel<EPI_STORE>, g4, dim3(256), 0, st, ws, split, d.M, d.N, d.C, d.ldc, d.sC, d.epi);
+        break;
+      case EPI_ACT:
+        hipLaunchKernelGGL(splitk_reduce4_kernel<EPI_ACT>, g4, dim3(256), 0, st, ws, split, d.M, d.N, d.C, d.ldc, d.sC, d.epi);
+        break;
+      case EPI_DACT:
+        hipLaunchKernelGGL(splitk_reduce4_kernel<EPI_DACT>, g4, dim3(256), 0, st, ws, split, d.M, d.N, d.C, d.ldc, d.sC, d.epi);
+        break;
+      case EPI_SIGMOID:
+        hipLaunchKernelGGL(splitk_reduce4_kernel<EPI_SIGMOID>, g4, dim3(256), 0, st, ws, split, d.M, d.N, d.C, d.ldc, d.sC, d.epi);
+        break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (d.epi.mode) {
     case EPI_STORE:
       hipLaunchKernelGGL(splitk_reduce_kernel<EPI_STORE>, g, dim3(256), 0, st, ws, split, d.M, d.N, d.C, d.ldc, d.sC, d.epi);

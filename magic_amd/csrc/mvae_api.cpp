@@ -66,8 +66,9 @@ struct mvae_ctx {
   struct PlaneBuf { float* base; size_t n; Planes pl; };
   std::vector<PlaneBuf> planes;
   int np = 0;            // planes per buffer: 0 (fp32 mode), 1 (bf16), 3 (f32x)
-  int* dyn = nullptr;    // f32x: residual planes of the de-interleaved pixels nonzero?
+  int* dyn = nullptr;    // bf16/f32x: some de-interleaved pixel not exact in bf16?
   int x32mask = 7;       // fp32 row blocks of xs the step reads (bit c: 0 rot, 1 lock, 2 key)
+  int x32dyn = 0;        // ... written only when *dyn != 0 (the BCE target, else read as bf16)
   // schedule (each GEMM tagged with its timing region)
   std::vector<GemmDesc> fwd_enc;  // encoder layers + head
   GemmDesc f_d1, f_d2, f_out;
@@ -446,7 +447,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     if (e == hipSuccess) e = add(c->dzd1, B * c->ld_d1);
     if (e == hipSuccess) e = add(c->dhead, 4 * B * c->ld_dh);
     for (int i = 0; e == hipSuccess && i < c->nenc; ++i) e = add(c->dzl[i], 4 * B * c->lddz);
-    if (e == hipSuccess && c->np == 3) e = dalloc(c, reinterpret_cast<float**>(&c->dyn), 4);
+    if (e == hipSuccess) e = dalloc(c, reinterpret_cast<float**>(&c->dyn), 4);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
       g_create_err = std::string("plane images: ") + hipGetErrorString(e);
@@ -461,7 +462,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     d.Ap = a.p; d.pA = a.stride; d.nA = c->np;
     d.Bp = b.p; d.pB = b.stride; d.nB = c->np;
     d.epi.cp = o.p; d.epi.pc = o.stride; d.epi.ncp = o.p ? c->np : 0;
-    d.dynA = (c->dyn && d.A >= c->xs && d.A < c->xs + (size_t)3 * B * c->ldx) ? c->dyn : nullptr;
+    d.dynA = (c->np == 3 && d.A >= c->xs && d.A < c->xs + (size_t)3 * B * c->ldx) ? c->dyn : nullptr;
     // exact split: GEMMs the 256x256 bf16 kernel does not serve (a dimension < 256: the
     // latent head, thin decoder layers) run faster as one native fp32 MFMA GEMM than as six
     // bf16 plane products on the 128x128 kernel; same accuracy class
@@ -472,12 +473,24 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   wire(c->f_d1);
   wire(c->f_d2);
   wire(c->f_out);
-  // fp32 xs rows: the BCE target (lock block) always; everything when a GEMM reads xs in fp32
+  // fp32 xs rows: everything when a GEMM reads xs in fp32; otherwise only the BCE target
+  // (lock block), and only for a batch whose pixels are not all bf16 values (the BCE epilogue
+  // reads plane 0 while *dyn == 0)
   if (c->np) {
-    c->x32mask = 2;
+    c->x32mask = 0;
+    c->x32dyn = 2;
     for (auto* v : {&c->fwd_enc, &c->bwd_enc})
       for (auto& d : *v)
         if (d.prec == GEMM_F32 && d.A >= c->xs && d.A < c->xs + (size_t)3 * B * c->ldx) c->x32mask = 7;
+    if (c->f_out.prec != GEMM_F32) {
+      const Planes xp = planes_of(c, c->xs);
+      c->f_out.epi.xp = xp.p + (size_t)B * c->ldx;
+      c->f_out.epi.xdyn = c->dyn;
+    } else {
+      c->x32mask |= 2;  // the native fp32 BCE GEMM reads the fp32 target rows
+    }
+    // dU feeds only the two decoder-output backward GEMMs: no fp32 copy when both read planes
+    c->f_out.epi.c32 = c->bwd_dec[0].prec != GEMM_F32 && c->bwd_dec[1].prec != GEMM_F32 ? 0 : 1;
   }
   for (auto* v : {&c->fwd_enc, &c->bwd_dec, &c->bwd_enc})
     for (auto& d : *v)
@@ -625,7 +638,7 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
     TIMED("deinterleave");
     if (c->dyn) MV_CHECK(hipMemsetAsync(c->dyn, 0, sizeof(int), st));
     MV_CHECK(launch_deinterleave(x, c->xs, planes_of(c, c->xs), c->dyn, c->B, c->D, c->ldx,
-                                 c->x32mask, st));
+                                 c->x32mask, c->x32dyn, st));
   }
   const size_t ne = (size_t)3 * c->B * c->L;
   {

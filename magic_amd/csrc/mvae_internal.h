@@ -13,6 +13,9 @@ enum EpiMode {
   EPI_DACT = 2,     // C = acc * act'(aux[remap(row)])  (dgrad through the producing activation)
   EPI_BCE = 3,      // sigmoid + reconstruction BCE row partials + dU = (y - x) * scale (+ optional y)
   EPI_SIGMOID = 4,  // C = sigmoid(acc)                 (generate / reconstruct)
+  EPI_BCEB = 5,     // EPI_BCE reading the target from its bf16 plane (kernel-internal: gemm_run
+                    // launches EPI_BCE and EPI_BCEB and each returns at once unless *xdyn
+                    // selects it -- a runtime choice inside one epilogue spills the accumulators)
 };
 
 enum Act { ACT_TANH = 0, ACT_ELU = 1 };
@@ -28,8 +31,12 @@ struct GemmEpi {
   int ld_aux = 0;
   int remap_split = 1 << 30;    // aux row = row >= remap_split ? row - remap_shift : row
   int remap_shift = 0;
-  const float* x = nullptr;     // BCE: target pixels (lock image)
+  const float* x = nullptr;     // BCE: target pixels (lock image), fp32
   int ldx = 0;
+  // BCE: bf16 plane 0 of the target (same ld). Read instead of x when *xdyn == 0, i.e. every
+  // pixel of the batch is exact in bf16; the fp32 rows are then never written.
+  const unsigned short* xp = nullptr;
+  const int* xdyn = nullptr;
   float scale = 1.f;            // BCE: 1/global_batch
   float* y = nullptr;           // BCE: optional sigmoid output
   int ldy = 0;
@@ -39,6 +46,7 @@ struct GemmEpi {
   unsigned short* cp = nullptr;
   long long pc = 0;
   int ncp = 0;
+  int c32 = 1;                  // 0: no fp32 C store (every consumer reads the planes)
 };
 
 // bf16 operand shadows (precision = bf16). When set, the GEMM reads A/B from these
@@ -81,9 +89,10 @@ struct Planes {
   int n = 0;
 };
 // f32mask: bit c -> write fp32 rows of block c (0 rot, 1 lock, 2 key). Plane 0 always (when
-// xp.p); with 3 planes, planes 1-2 are written only when *dyn ends up nonzero.
+// xp.p); *dyn (zeroed by the caller) is set when a pixel is not a bf16 value, and only then
+// are planes 1-2 (3-plane mode) and the fp32 rows of the blocks in f32dyn_mask written.
 hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int B, int D,
-                               int ldx, int f32mask, hipStream_t st);
+                               int ldx, int f32mask, int f32dyn_mask, hipStream_t st);
 hipError_t launch_normal(float* out, size_t n, uint64_t seed, uint64_t counter, hipStream_t st);
 hipError_t launch_latent_fwd(const float* ms, const float* eps, float* z, const Planes& zp, int B,
                              int L, int ldz, hipStream_t st);

@@ -105,9 +105,12 @@ __global__ void deinterleave_scalar_kernel(const float* __restrict__ x, float* _
   if (dyn && __ballot(nz) != 0 && (threadIdx.x & 63) == 0) atomicOr(dyn, 1);
 }
 
-// planes 1 and 2 of the exact split of the layer-0 operand, only when *dyn != 0
-__global__ void residual_planes_kernel(const float* __restrict__ x, unsigned short* __restrict__ xp,
-                                       long long ps, const int* __restrict__ dyn, int B, int D,
+// Only when *dyn != 0 (some pixel of the batch is not a bf16 value): planes 1 and 2 of the
+// exact split of the layer-0 operand (3-plane mode), and the fp32 rows of the blocks in
+// f32mask (the BCE target, read from bf16 plane 0 while every pixel is exact).
+__global__ void residual_planes_kernel(const float* __restrict__ x, float* __restrict__ xs,
+                                       unsigned short* __restrict__ xp, long long ps, int np,
+                                       int f32mask, const int* __restrict__ dyn, int B, int D,
                                        int ldx) {
   if (*dyn == 0) return;
   const size_t n = (size_t)B * D;
@@ -119,10 +122,13 @@ __global__ void residual_planes_kernel(const float* __restrict__ x, unsigned sho
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const size_t o = (size_t)(c * B + b) * ldx + p;
-      float r1, r2, r3;
-      (void)bf16_rn(v[c], r1);
-      xp[ps + o] = bf16_rn(r1, r2);
-      xp[2 * ps + o] = bf16_rn(r2, r3);
+      if (f32mask >> c & 1) xs[o] = v[c];
+      if (np == 3) {
+        float r1, r2, r3;
+        (void)bf16_rn(v[c], r1);
+        xp[ps + o] = bf16_rn(r1, r2);
+        xp[2 * ps + o] = bf16_rn(r2, r3);
+      }
     }
   }
 }
@@ -449,7 +455,7 @@ inline unsigned nblocks(size_t n, int bs) { return (unsigned)((n + bs - 1) / bs)
 }  // namespace
 
 hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int B, int D,
-                               int ldx, int f32mask, hipStream_t st) {
+                               int ldx, int f32mask, int f32dyn_mask, hipStream_t st) {
   if ((D % 4) == 0 && (reinterpret_cast<uintptr_t>(x) % 16) == 0 && (ldx % 4) == 0) {
     dim3 g(nblocks(D / 4, 256), B);
     hipLaunchKernelGGL(deinterleave_vec_kernel, g, dim3(256), 0, st,
@@ -459,9 +465,10 @@ hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int*
     hipLaunchKernelGGL(deinterleave_scalar_kernel, g, dim3(256), 0, st, x, xs, xp.p, dyn, B, D, ldx,
                        f32mask);
   }
-  if (xp.n == 3 && dyn)
-    hipLaunchKernelGGL(residual_planes_kernel, dim3(2048), dim3(256), 0, st, x, xp.p, xp.stride, dyn,
-                       B, D, ldx);
+  f32dyn_mask &= ~f32mask;
+  if (dyn && xp.p && (xp.n == 3 || f32dyn_mask))
+    hipLaunchKernelGGL(residual_planes_kernel, dim3(2048), dim3(256), 0, st, x, xs, xp.p, xp.stride,
+                       xp.n, f32dyn_mask, dyn, B, D, ldx);
   return hipGetLastError();
 }
 

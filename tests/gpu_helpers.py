@@ -17,10 +17,13 @@ def oracle_cfg(cfg: MVAEConfig) -> O.OracleConfig:
                           beta1=cfg.beta1, beta2=cfg.beta2, epsilon=cfg.epsilon)
 
 
-def make_inputs(cfg: MVAEConfig, B: int, seed: int = 1, density: float = 0.1):
-    """Binary pixels (HWC-interleaved), areas in the reference's range, eps [3,B,L]."""
+def make_inputs(cfg: MVAEConfig, B: int, seed: int = 1, density: float = 0.1, grey: bool = False):
+    """Binary pixels (HWC-interleaved), areas in the reference's range, eps [3,B,L].
+    grey: foreground pixels take k/255 values (not exact in bf16: the fp32-target paths)."""
     rng = np.random.default_rng(seed)
     X = (rng.random((B, 3 * cfg.D)) < density).astype(np.float32)
+    if grey:
+        X *= (rng.integers(1, 256, size=X.shape) / 255.0).astype(np.float32)
     areas = rng.integers(296, 6427, size=B).astype(np.float32)
     eps = np.random.default_rng(seed + 1).standard_normal((3, B, cfg.latent)).astype(np.float32)
     return X, areas, eps

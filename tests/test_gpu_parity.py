@@ -145,24 +145,35 @@ FLAVOURS = [
 ]
 
 
-def check_step(cfg, seed=1, density=0.1, tol=TOL, adam=True):
+def check_step(cfg, seed=1, density=0.1, tol=TOL, adam=True, grey=False, loss_tol=None,
+               dist_tol=None, recon=False):
+    """One step vs the oracle. tol: gradients (and losses / distance unless loss_tol /
+    dist_tol are given); recon: also mvae_reconstruct's y vs the oracle's decoder output."""
+    loss_tol = tol if loss_tol is None else loss_tol
+    dist_tol = tol if dist_tol is None else dist_tol
     eng = _engine(cfg)
     try:
         P = make_params(cfg)
         eng.load_params(P)
-        X, areas, eps = make_inputs(cfg, cfg.batch, seed=seed, density=density)
+        X, areas, eps = make_inputs(cfg, cfg.batch, seed=seed, density=density, grey=grey)
+        y = eng.reconstruct(to_dev(X), to_dev(eps)).cpu().numpy() if recon else None
         lg, dg, g1g, g2g = gpu_phases(eng, X, areas, eps)
+        dyn = int(eng.buffer(_lib.BUF_DYN).view(torch.int32).item()) if cfg.precision != "f32" else None
         lo, do, g1o, g2o, oc_cache = oracle_phases(cfg, P, X, areas, eps)
         m1, m2 = oc_cache["mag"]
+        if dyn is not None:
+            assert dyn == int(grey), ("dyn flag", dyn, grey)
         for i, nm in enumerate(("cost", "training_loss", "r_l", "l_l", "d_l")):
-            assert abs(lg[i] - lo[i]) <= tol * max(abs(lo[i]), 1e-3), (nm, lg[i], lo[i])
-        assert max_rel(dg, do) <= tol, ("distance", max_rel(dg, do))
+            assert abs(lg[i] - lo[i]) <= loss_tol * max(abs(lo[i]), 1e-3), (nm, lg[i], lo[i])
+        assert max_rel(dg, do) <= dist_tol, ("distance", max_rel(dg, do))
         for k in O.trained_names(oracle_cfg(cfg)):
             e = max_rel(g1g[k], g1o[k], m1[k])
             assert e <= tol, ("g1", k, e)
         for k in O.encoder_names(oracle_cfg(cfg)):
             e = max_rel(g2g[k], g2o[k], m2[k])
             assert e <= tol, ("g2", k, e)
+        if recon:
+            assert max_rel(y, oc_cache["y"]) <= dist_tol, ("reconstruct", max_rel(y, oc_cache["y"]))
         assert set(g2g) == set(O.encoder_names(oracle_cfg(cfg)))
         if adam:
             # Adam kernel vs TF ApplyAdam restated, both fed the GPU's own gradients (the
@@ -397,3 +408,60 @@ def test_step_bf16_documented_tolerance():
         assert worst <= 5e-2, worst
     finally:
         eng.close()
+
+
+# ------------------------------------------------------------------ 256x256 kernel paths
+@pytest.mark.parametrize("prec", [2, 1], ids=["f32x", "bf16"])
+@pytest.mark.parametrize("epi,act", [(1, 0), (1, 1), (2, 0), (2, 1), (4, 0)])
+@pytest.mark.parametrize("M,N,ldc", [(600, 520, 520), (300, 500, 500), (513, 257, 260), (280, 300, 301)])
+def test_gemm_wide_epilogues(prec, epi, act, M, N, ldc):
+    """Fused epilogues of the 256x256 kernel (LDS-transposed 16-B row stores; scalar tails on
+    ragged columns and unaligned rows) against float64; nothing written past column N."""
+    lib = _lib.load()
+    K = 304
+    g = torch.Generator(device="cuda").manual_seed(M + 7 * N + 31 * epi + act)
+    A = torch.randn(M, K, device="cuda", generator=g) * 0.3
+    Bm = _padded(K, N, g) * 0.3
+    ld_aux = (N + 7) // 8 * 8
+    pre = torch.randn(M, ld_aux, device="cuda", generator=g)
+    aux = torch.tanh(pre) if act == 0 else torch.nn.functional.elu(pre)
+    C = torch.full((M, ldc), float("nan"), device="cuda")
+    rc = lib.mvae_debug_gemm(M, N, K, A.data_ptr(), K, 0, Bm.data_ptr(), Bm.shape[1], 0, C.data_ptr(),
+                             ldc, epi | (prec << 4), act, aux.data_ptr(), ld_aux,
+                             torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, lib.mvae_last_error(None)
+    acc = A.double() @ Bm[:, :N].double()
+    a = aux[:, :N].double()
+    if epi == 1:
+        ref = torch.tanh(acc) if act == 0 else torch.where(acc < 0, torch.exp(acc) - 1, acc)
+    elif epi == 2:
+        ref = acc * (1 - a * a) if act == 0 else torch.where(a < 0, acc * (a + 1), acc)
+    else:
+        ref = torch.sigmoid(acc)
+    mag = (A.double().abs() @ Bm[:, :N].double().abs()).max().item()
+    bound = (2e-6 if prec == 2 else 1e-2) * mag + 1e-6
+    err = (C[:, :N].double() - ref).abs().max().item()
+    assert err <= bound, (err, bound)
+    if ldc > N:
+        assert torch.isnan(C[:, N:]).all()
+
+
+@pytest.mark.parametrize("prec", ["f32x", "bf16"])
+@pytest.mark.parametrize("grey", [False, True], ids=["binary", "grey"])
+def test_step_wide_kernels(prec, grey):
+    """Batch 288 of 20x20 images with 300/260/280-wide encoder layers: every encoder and
+    decoder GEMM with both dimensions >= 256 runs on the 256x256 kernel with its fused
+    epilogue (BCE row partials and dU planes without an fp32 copy, DACT row remap, ACT planes,
+    vectorised split-K reductions). Binary pixels: BCE target read from its bf16 plane and 3
+    plane pairs for the layer-0 products (f32x); grey pixels: fp32 target rows and 6 pairs."""
+    cfg = preset("8c", image_size=20, batch=288, precision=prec).replace(enc=(300, 260, 280))
+    if prec == "f32x":
+        check_step(cfg, grey=grey, recon=True)
+    else:  # documented bf16 tolerance (test_step_bf16_documented_tolerance)
+        check_step(cfg, grey=grey, tol=5e-2, loss_tol=2e-3, dist_tol=2e-2, recon=True)
+
+
+def test_step_c2_f32x_full_size():
+    """The benched configuration itself (BASELINE C2 as bench.py runs it: f32x, B=4096, 100x100,
+    enc [500]*4, L=20) against float64 at the fp32 bar."""
+    check_step(preset("8c", image_size=100, batch=4096, precision="f32x"), adam=False)
