@@ -409,6 +409,142 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16w_kernel(PParams pp) {
   epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
 }
 
+// ---------------------------------------------------------------------------------------
+// Ring form of the wide kernel (same 256x256x64 tile, waves, fragments and epilogue). The
+// k-loop walks (k-tile, plane pair) with the pairs INNERMOST, and the A and B operand images
+// live in LDS rings of 3 and 2 slots (5 x 32 KB = the CU's 160 KB): an image is copied only
+// when the iteration's (plane, k-tile) differs from the previous iteration's. The split's
+// pairs are ordered (0,0) (0,1) (0,2) (1,0) (1,1) (2,0), so with binary pixels (pairs with
+// i = 0 only) the layer-0 operand is copied once per k-tile instead of once per pair, and with
+// six pairs A is copied 3 and B 6 times per k-tile instead of 6 + 6.
+// Pipeline: iteration it opens with a counted vmcnt (its B image, issued in it-1, and its A
+// image, issued in it-2, have landed; the A copy for it+1 stays in flight across the barrier)
+// and a raw s_barrier; it then issues the B copy for it+1 and, after its first k16-step, the
+// A copy for it+2, each into a ring slot whose last reader finished before the barrier.
+// SP: s_setprio 1 around each MFMA cluster (cdna_hip_programming.md T5).
+template <bool AT, bool BT, int EPI, bool SP>
+__global__ __launch_bounds__(WNT, 1) void gemm_bf16r_kernel(PParams pp) {
+  constexpr int BK = 64;
+  constexpr int IMG = WT * BK;  // bf16 elements per operand image
+  const Params& p = pp.g;
+  if (epi_skip<EPI>(p.epi)) return;
+  __shared__ __attribute__((aligned(16))) short smem[5 * IMG];  // A slots 0-2 | B slots 0-1
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const Tile t = tile_of_t<WT, WT>(p, true);
+  const unsigned short* __restrict__ A = pp.A + t.bi * p.sA;
+  const unsigned short* __restrict__ Bm = pp.B + t.bi * p.sB;
+
+  WLoad<!AT, BK> la;
+  WLoad<BT, BK> lb;
+  la.init(p.lda, t.m0, p.M, wave, lane);
+  lb.init(p.ldb, t.n0, p.N, wave, lane);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int np = (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
+  const int nkt = t.ks < t.ke ? (t.ke - t.ks + BK - 1) / BK : 0;
+  const int total = np * nkt;
+  constexpr int NRD = 4 * WLoad<!AT, BK>::NRD + 2 * WLoad<BT, BK>::NRD;  // LDS reads / k16-step
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
+
+  // cursors: (k-tile, pair) of iterations it (cur), it+1 (n1) and it+2 (n2)
+  auto adv = [&](int& kt, int& pr) { if (++pr == np) { pr = 0; ++kt; } };
+  auto pa_of = [&](int pr) { return (pp.pab >> (4 * pr)) & 3; };
+  auto pb_of = [&](int pr) { return (pp.pab >> (4 * pr + 2)) & 3; };
+  int kt0 = 0, pr0 = 0, kt1 = 0, pr1 = 0, kt2 = 0, pr2 = 0;
+  adv(kt1, pr1);
+  adv(kt2, pr2); adv(kt2, pr2);
+  // ring slots of the images of it, it+1, it+2 (A) and it, it+1 (B)
+  int sa0 = 0, sa1 = 0, sa2 = 0, sb0 = 0;
+  bool na1 = false;  // A image of it+1 is a new copy (issued, possibly still in flight)
+  if (total > 0) {
+    la.issue(A + pa_of(0) * pp.pA, p.lda, t.ks, t.ke, smem, wave);
+    lb.issue(Bm + pb_of(0) * pp.pB, p.ldb, t.ks, t.ke, smem + 3 * IMG, wave);
+    if (total > 1) {
+      na1 = kt1 != kt0 || pa_of(pr1) != pa_of(pr0);
+      sa1 = na1 ? 1 : 0;
+      if (na1) la.issue(A + pa_of(pr1) * pp.pA, p.lda, t.ks + kt1 * BK, t.ke, smem + IMG, wave);
+    }
+  }
+  for (int it = 0; it < total; ++it) {
+    // images of it landed (this wave's copies), then for every wave
+    if (na1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    // B copy for it+1 (needed first), A copy for it+2 (after the first k16-step)
+    const bool nb1 = it + 1 < total && (kt1 != kt0 || pb_of(pr1) != pb_of(pr0));
+    const int sb1 = nb1 ? sb0 ^ 1 : sb0;
+    if (nb1) lb.issue(Bm + pb_of(pr1) * pp.pB, p.ldb, t.ks + kt1 * BK, t.ke,
+                      smem + (3 + sb1) * IMG, wave);
+    const bool na2 = it + 2 < total && (kt2 != kt1 || pa_of(pr2) != pa_of(pr1));
+    sa2 = na2 ? (sa1 == 2 ? 0 : sa1 + 1) : sa1;
+    const short* sa = smem + sa0 * IMG;
+    const short* sb = smem + (3 + sb0) * IMG;
+    const unsigned la0 = lds0 + 2u * (unsigned)(sa0 * IMG);
+    const unsigned lb0 = lds0 + 2u * (unsigned)((3 + sb0) * IMG);
+    bf16x8 fa[2][4], fb[2][2];
+    auto rd = [&](int ks, bf16x8 (&a)[4], bf16x8 (&b)[2]) {
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) b[ni] = lb.frag(sb, lb0, wn * 64 + ni * 32, ks, lane);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) a[mi] = la.frag(sa, la0, wm * 128 + mi * 32, ks, lane);
+    };
+    rd(0, fa[0], fb[0]);
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      if (ks + 1 < BK / 16) {
+        rd(ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
+        wait_lds<NRD>();
+      } else {
+        wait_lds<0>();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (SP) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks & 1][mi], fb[ks & 1][ni],
+                                                                acc[mi][ni], 0, 0, 0);
+      if constexpr (SP) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks == 0 && na2)
+        la.issue(A + pa_of(pr2) * pp.pA, p.lda, t.ks + kt2 * BK, t.ke, smem + sa2 * IMG, wave);
+    }
+    // shift the cursors
+    sa0 = sa1; sa1 = sa2; sb0 = sb1; na1 = na2;
+    kt0 = kt1; pr0 = pr1; kt1 = kt2; pr1 = pr2; adv(kt2, pr2);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
+}
+
+template <bool AT, bool BT, int EPI, bool SP>
+hipError_t launch_r(const PParams& p, hipStream_t st) {
+  const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
+  hipLaunchKernelGGL((gemm_bf16r_kernel<AT, BT, EPI, SP>), dim3(nwg), dim3(WNT), 0, st, p);
+  return hipGetLastError();
+}
+
+template <int EPI, bool SP>
+hipError_t launch_ring_t(const PParams& p, bool at, bool bt, hipStream_t st) {
+  if (!at && !bt) return launch_r<false, false, EPI, SP>(p, st);
+  if (at && !bt) return launch_r<true, false, EPI, SP>(p, st);
+  if (!at && bt) return launch_r<false, true, EPI, SP>(p, st);
+  return launch_r<true, true, EPI, SP>(p, st);
+}
+
 template <bool AT, bool BT, int EPI, int BK, int DEPTH>
 hipError_t launch_w(const PParams& p, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
@@ -424,13 +560,18 @@ hipError_t launch_wide_t(const PParams& p, bool at, bool bt, hipStream_t st) {
   return launch_w<true, true, EPI, BK, DEPTH>(p, st);
 }
 
-// wide variants (diagnostics): 5 = BK 32 x 4 stages; otherwise BK 64 x 2 stages
+// wide variants (diagnostics, EPI_STORE): 5 = two-stage form at BK 32 x 4 stages, 7 = ring form
+// with s_setprio, 8 = two-stage form at BK 64 x 2 stages; otherwise (0, 3, 6) the ring form
 template <int EPI>
 hipError_t launch_wide(const PParams& p, bool at, bool bt, int variant, hipStream_t st) {
   if constexpr (EPI == EPI_STORE) {
     if (variant == 5) return launch_wide_t<EPI, 32, 4>(p, at, bt, st);
+    if (variant == 7) return launch_ring_t<EPI, true>(p, at, bt, st);
+    if (variant == 8) return launch_wide_t<EPI, 64, 2>(p, at, bt, st);
   }
-  return launch_wide_t<EPI, 64, 2>(p, at, bt, st);
+  // default: the ring form (profiles/r1/gemm_ab_ring.txt: +3..28 % over the two-stage form
+  // on the step's shapes; s_setprio around the MFMA clusters measured neutral)
+  return launch_ring_t<EPI, false>(p, at, bt, st);
 }
 
 template <bool AT, bool BT, int EPI, int BK, bool DB>
@@ -466,7 +607,7 @@ hipError_t launch_var(const PParams& p, bool at, bool bt, int variant, hipStream
 bool gemm_bf16_wide(const GemmDesc& d) {
   if (d.prec == GEMM_F32) return false;
   if (d.variant == 1 || d.variant == 2 || d.variant == 4) return false;  // 128x128 variants
-  if (d.variant != 3 && d.variant != 5 && (d.M < 256 || d.N < 256)) return false;
+  if (d.variant != 3 && d.variant < 5 && (d.M < 256 || d.N < 256)) return false;
   auto a8 = [](long long v) { return (v & 7) == 0; };
   if (!a8(d.lda) || !a8(d.ldb) || !a8(d.pA) || !a8(d.pB)) return false;
   if (d.batch > 1 && (!a8(d.sA) || !a8(d.sB))) return false;

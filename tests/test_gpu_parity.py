@@ -66,10 +66,13 @@ def _padded(rows, cols, g):
 @pytest.mark.parametrize("prec", [2, 1], ids=["f32x", "bf16"])
 @pytest.mark.parametrize("at,bt", [(0, 0), (1, 0), (0, 1), (1, 1)])
 @pytest.mark.parametrize("M,N,K,variant", [(256, 256, 64, 3), (300, 517, 1001, 3), (1000, 600, 4099, 0),
-                                           (513, 260, 130, 0), (40, 70, 200, 3)])
+                                           (513, 260, 130, 0), (40, 70, 200, 3), (1000, 600, 4099, 8),
+                                           (300, 517, 1001, 7), (513, 260, 130, 7), (40, 70, 200, 7),
+                                           (256, 256, 64, 7)])
 def test_gemm_wide_kernel(at, bt, M, N, K, variant, prec):
     """The 256x256 LDS-DMA bf16 kernel (variant 3 forces it; 0 lets the planner pick it for
-    M, N >= 256) on every layout, ragged edges and split-K, against float64."""
+    M, N >= 256: the operand-ring form; 7 adds s_setprio, 8 is the two-stage form) on every layout,
+    ragged edges and split-K, against float64."""
     lib = _lib.load()
     g = torch.Generator(device="cuda").manual_seed(M * 5 + N * 11 + K)
     A = _padded(K, M, g) if at else _padded(M, K, g)
