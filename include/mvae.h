@@ -157,6 +157,9 @@ int mvae_make_batch(const unsigned char* locks, const unsigned char* keys, int h
 /* HIP-event timing of named regions (one GEMM incl. its split-K reduction, or one
  * bandwidth kernel group), recorded on the launch stream while enabled.               */
 int mvae_timing_enable(mvae_ctx* ctx, int on);
+/* Restrict recording to one region (-1: all regions, the default): a timed loop can carry the
+   events of the one kernel it reports without the event pairs of every other region. */
+int mvae_timing_select(mvae_ctx* ctx, int region);
 int mvae_timing_regions(mvae_ctx* ctx);
 const char* mvae_timing_name(mvae_ctx* ctx, int region);
 int mvae_timing_read(mvae_ctx* ctx, int region, double* total_ms, int64_t* count);

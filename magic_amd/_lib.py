@@ -76,6 +76,7 @@ _SIGS = {
     "mvae_make_batch": ([C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
                          C.c_void_p, C.c_void_p], C.c_int),
     "mvae_timing_enable": ([C.c_void_p, C.c_int], C.c_int),
+    "mvae_timing_select": ([C.c_void_p, C.c_int], C.c_int),
     "mvae_timing_regions": ([C.c_void_p], C.c_int),
     "mvae_timing_name": ([C.c_void_p, C.c_int], C.c_char_p),
     "mvae_timing_read": ([C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)], C.c_int),

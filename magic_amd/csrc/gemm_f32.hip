@@ -385,7 +385,8 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   }
   // split-K: raw slabs [batch][split][M][N], then ordered reduction + epilogue
   p.C = ws; p.ldc = d.N; p.sC = (long long)d.M * d.N;
-  p.epi.cp = nullptr;  // planes are written by the reduction
+  p.epi.cp = nullptr;  // planes (and the fp32 output, if any) are written by the reduction
+  p.epi.c32 = 1;       // the slabs themselves always
   hipError_t err = d.prec != GEMM_F32 ? gemm_bf16_launch(p, d, EPI_STORE, st)
                                       : launch_store(p, d.at, d.bt, d.variant, st);
   if (err != hipSuccess) return err;

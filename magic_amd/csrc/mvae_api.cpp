@@ -84,6 +84,7 @@ struct mvae_ctx {
   std::vector<Pending> pending;
   std::vector<hipEvent_t> event_pool;
   bool timing = false;
+  int timing_sel = -1;   // record only this region (-1: all)
   // optimizer state (TF beta1_power / beta2_power are fp32 variables)
   int64_t t1 = 0, t2 = 0;
   float b1p[2] = {0, 0}, b2p[2] = {0, 0};
@@ -165,7 +166,10 @@ static hipEvent_t take_event(mvae_ctx* c) {
 struct TimeScope {
   mvae_ctx* c; int r; hipStream_t st; hipEvent_t a = nullptr;
   TimeScope(mvae_ctx* c_, int r_, hipStream_t st_) : c(c_), r(r_), st(st_) {
-    if (c->timing) { a = take_event(c); (void)hipEventRecord(a, st); }
+    if (c->timing && (c->timing_sel < 0 || c->timing_sel == r)) {
+      a = take_event(c);
+      (void)hipEventRecord(a, st);
+    }
   }
   ~TimeScope() {
     if (a) {
@@ -489,8 +493,26 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     } else {
       c->x32mask |= 2;  // the native fp32 BCE GEMM reads the fp32 target rows
     }
-    // dU feeds only the two decoder-output backward GEMMs: no fp32 copy when both read planes
-    c->f_out.epi.c32 = c->bwd_dec[0].prec != GEMM_F32 && c->bwd_dec[1].prec != GEMM_F32 ? 0 : 1;
+    // fp32 copies only of the GEMM outputs something reads in fp32: an operand of a native
+    // fp32 GEMM or the aux of a DACT epilogue (e.g. dU and the dgrads feeding plane GEMMs
+    // only are written as planes alone). Outputs without a plane image keep their fp32 store.
+    std::vector<GemmDesc*> all;
+    for (auto* v : {&c->fwd_enc, &c->bwd_dec, &c->bwd_enc})
+      for (auto& d : *v) all.push_back(&d);
+    for (GemmDesc* d : {&c->f_d1, &c->f_d2, &c->f_out}) all.push_back(d);
+    for (GemmDesc* d : all) {
+      const mvae_ctx::PlaneBuf* pb = nullptr;
+      for (const auto& q : c->planes)
+        if (d->C >= q.base && d->C < q.base + q.n) pb = &q;
+      if (!pb || !d->epi.cp) continue;
+      auto in = [&](const float* x) { return x && x >= pb->base && x < pb->base + pb->n; };
+      bool fp32_reader = false;
+      for (const GemmDesc* g : all) {
+        if (g->prec == GEMM_F32 && (in(g->A) || in(g->B))) fp32_reader = true;
+        if (g->epi.mode == EPI_DACT && in(g->epi.aux)) fp32_reader = true;
+      }
+      d->epi.c32 = fp32_reader ? 1 : 0;
+    }
   }
   for (auto* v : {&c->fwd_enc, &c->bwd_dec, &c->bwd_enc})
     for (auto& d : *v)
@@ -891,6 +913,12 @@ extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int
 extern "C" int mvae_timing_enable(mvae_ctx* ctx, int on) {
   if (!ctx) return MVAE_EINVAL;
   ctx->timing = on != 0;
+  return MVAE_OK;
+}
+
+extern "C" int mvae_timing_select(mvae_ctx* ctx, int region) {
+  if (!ctx || region < -1 || region >= (int)ctx->region_names.size()) return MVAE_EINVAL;
+  ctx->timing_sel = region;
   return MVAE_OK;
 }
 

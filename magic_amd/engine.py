@@ -232,6 +232,15 @@ class Engine:
     def timing_enable(self, on: bool = True):
         self._check(self.lib.mvae_timing_enable(self.ctx, int(on)))
 
+    def timing_select(self, name: Optional[str] = None):
+        """Record only region ``name`` (None: all regions)."""
+        r = -1
+        if name is not None:
+            names = [self.lib.mvae_timing_name(self.ctx, i).decode()
+                     for i in range(self.lib.mvae_timing_regions(self.ctx))]
+            r = names.index(name)
+        self._check(self.lib.mvae_timing_select(self.ctx, r))
+
     def timing_reset(self):
         self._check(self.lib.mvae_timing_reset(self.ctx))
 
