@@ -608,6 +608,10 @@ bool gemm_bf16_wide(const GemmDesc& d) {
   if (d.prec == GEMM_F32) return false;
   if (d.variant == 1 || d.variant == 2 || d.variant == 4) return false;  // 128x128 variants
   if (d.variant != 3 && d.variant < 5 && (d.M < 256 || d.N < 256)) return false;
+  // one k-tile and under a CU's worth of 256x256 tiles (dec layer 1: K = L + 1; the head's
+  // dgrad: K = 2L): epilogue-bound on few CUs, the 128x128 kernels spread it wider
+  const long long t256 = (long long)((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
+  if (d.variant == 0 && d.K <= 64 && t256 < 256) return false;
   auto a8 = [](long long v) { return (v & 7) == 0; };
   if (!a8(d.lda) || !a8(d.ldb) || !a8(d.pA) || !a8(d.pB)) return false;
   if (d.batch > 1 && (!a8(d.sA) || !a8(d.sB))) return false;

@@ -269,6 +269,29 @@ def test_determinism_bitwise():
         eng.close()
 
 
+def test_determinism_bitwise_f32x_splitk():
+    """f32x at a size where the 256x256 GEMMs split K (slabs summed in slice order by the
+    reduction kernel): bitwise identical across runs."""
+    cfg = preset("8c", image_size=40, batch=768, precision="f32x").replace(enc=(400, 300))
+    eng = _engine(cfg)
+    try:
+        P = make_params(cfg)
+        X, areas, eps = make_inputs(cfg, cfg.batch)
+        outs = []
+        for _ in range(3):
+            eng.load_params(P)
+            outs.append(gpu_phases(eng, X, areas, eps))
+        for o in outs[1:]:
+            for a, b in zip(outs[0][:2], o[:2]):
+                np.testing.assert_array_equal(a, b)
+            for k in outs[0][2]:
+                np.testing.assert_array_equal(outs[0][2][k], o[2][k])
+            for k in outs[0][3]:
+                np.testing.assert_array_equal(outs[0][3][k], o[3][k])
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("n_enc", [1, 3])
 def test_backward_parts_match_backward(n_enc):
     """backward_part(0..2) == backward bitwise; the released ranges tile g1 and the encoder
