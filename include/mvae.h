@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MVAE_ABI_VERSION 1
+#define MVAE_ABI_VERSION 2
 #define MVAE_MAX_ENC 8
 
 enum { MVAE_OK = 0, MVAE_EINVAL = -1, MVAE_ECONFIG = -2, MVAE_ESTATE = -3 };
@@ -112,6 +112,16 @@ int mvae_buffer(mvae_ctx* ctx, int which, float** ptr, size_t* count);
 /* Optimizer step counters (TF beta1_power/beta2_power, kept on the host in fp32). */
 int mvae_get_step(mvae_ctx* ctx, int64_t* t1, int64_t* t2);
 int mvae_set_step(mvae_ctx* ctx, int64_t t1, int64_t t2);
+/* Philox call counters of the internal N(0,1) sampler (eps == NULL): training draws
+ * (mvae_forward / mvae_train_step) and inference draws (mvae_predict / mvae_reconstruct)
+ * are separate streams, so evaluation never shifts the training noise; save both with a
+ * checkpoint to resume the exact sequence. Counters must be < 2^63. */
+/* Data parallelism: this rank's rows start at row_offset of the global batch (default 0).
+ * The internal sampler then draws exactly this rank's slice of the eps a single process
+ * would draw for the whole global batch. 0 <= row_offset <= global_batch - batch. */
+int mvae_set_shard(mvae_ctx* ctx, int64_t row_offset);
+int mvae_get_rng(mvae_ctx* ctx, uint64_t* train, uint64_t* eval);
+int mvae_set_rng(mvae_ctx* ctx, uint64_t train, uint64_t eval);
 /* Re-derive the bf16 plane images of the parameters from the fp32 masters: call after
  * writing parameters through mvae_param_info views (bf16 / f32x modes; no-op for f32). */
 int mvae_sync_params(mvae_ctx* ctx, void* stream);
@@ -140,6 +150,7 @@ int mvae_train_step(mvae_ctx* ctx, const float* x, const float* areas, const flo
 
 /* ---- inference surface ------------------------------------------------------------ */
 int mvae_predict(mvae_ctx* ctx, const float* x, const float* eps, float* dist_out, void* stream);
+/* transform: the lock image's latent mean only (no eps draw). */
 int mvae_transform(mvae_ctx* ctx, const float* x, float* zmean_out, void* stream);
 int mvae_reconstruct(mvae_ctx* ctx, const float* x, const float* eps, float* y_out, void* stream);
 /* z: [n, L] (n <= B) -> y: [n, D] */
@@ -149,9 +160,11 @@ int mvae_generate(mvae_ctx* ctx, const float* z, int n, float* y_out, void* stre
 /* locks, keys: uint8 [n][H][W] (decoded PNGs, 0..255) on the device; idx: int [B] example
  * of each row; coef: float [B][4] = (cos, sin, x_off, y_off) of each row's rotation
  * (tf.contrib.image.rotate, computed on the host in fp32, 16-byte aligned).
- * Writes x_out [B, H*W*3] float32: per pixel (lock, rotated lock, key) / 255.            */
+ * Writes x_out [B, H*W*3] float32: per pixel (lock, rotated lock, key) / divisor
+ * (255: inputs(normalize=True), 11a/overlap_input.py:113-115; 1: raw 0..255 pixels).       */
 int mvae_make_batch(const unsigned char* locks, const unsigned char* keys, int height, int width,
-                    const int* idx, const float* coef, int batch, float* x_out, void* stream);
+                    const int* idx, const float* coef, int batch, float divisor, float* x_out,
+                    void* stream);
 
 /* ---- diagnostics ------------------------------------------------------------------ */
 /* HIP-event timing of named regions (one GEMM incl. its split-K reduction, or one
@@ -160,6 +173,10 @@ int mvae_timing_enable(mvae_ctx* ctx, int on);
 /* Restrict recording to one region (-1: all regions, the default): a timed loop can carry the
    events of the one kernel it reports without the event pairs of every other region. */
 int mvae_timing_select(mvae_ctx* ctx, int region);
+/* Profiler runs: bracket every launch of `region` with an empty marker kernel of
+ * 4096 + region workgroups, so a rocprofv3 kernel trace can attribute dispatches (and their
+ * counters) to the region. Off by default. */
+int mvae_timing_marker(mvae_ctx* ctx, int region, int on);
 int mvae_timing_regions(mvae_ctx* ctx);
 const char* mvae_timing_name(mvae_ctx* ctx, int region);
 int mvae_timing_read(mvae_ctx* ctx, int region, double* total_ms, int64_t* count);

@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MVAE_LIB", os.path.join(HERE, "libmvae.so"))
 
 MVAE_MAX_ENC = 8
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 ACT = {"tanh": 0, "elu": 1}
 METRIC = {"cosine": 0, "sqdiff": 1}
@@ -60,6 +60,9 @@ _SIGS = {
     "mvae_buffer": ([C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)], C.c_int),
     "mvae_get_step": ([C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int64)], C.c_int),
     "mvae_set_step": ([C.c_void_p, C.c_int64, C.c_int64], C.c_int),
+    "mvae_set_shard": ([C.c_void_p, C.c_int64], C.c_int),
+    "mvae_get_rng": ([C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)], C.c_int),
+    "mvae_set_rng": ([C.c_void_p, C.c_uint64, C.c_uint64], C.c_int),
     "mvae_sync_params": ([C.c_void_p, C.c_void_p], C.c_int),
     "mvae_forward": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mvae_metric": ([C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
@@ -74,9 +77,10 @@ _SIGS = {
     "mvae_reconstruct": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mvae_generate": ([C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p], C.c_int),
     "mvae_make_batch": ([C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_int,
-                         C.c_void_p, C.c_void_p], C.c_int),
+                         C.c_float, C.c_void_p, C.c_void_p], C.c_int),
     "mvae_timing_enable": ([C.c_void_p, C.c_int], C.c_int),
     "mvae_timing_select": ([C.c_void_p, C.c_int], C.c_int),
+    "mvae_timing_marker": ([C.c_void_p, C.c_int, C.c_int], C.c_int),
     "mvae_timing_regions": ([C.c_void_p], C.c_int),
     "mvae_timing_name": ([C.c_void_p, C.c_int], C.c_char_p),
     "mvae_timing_read": ([C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_int64)], C.c_int),

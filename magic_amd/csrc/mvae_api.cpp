@@ -31,6 +31,8 @@ struct Block {
 
 inline int round8(int v) { return (v + 7) & ~7; }
 inline size_t align64(size_t v) { return (v + 63) & ~size_t(63); }
+// Philox call counters of inference draws carry this bit (a stream disjoint from training's)
+constexpr uint64_t EVAL_STREAM = 1ull << 63;
 
 }  // namespace
 
@@ -85,10 +87,14 @@ struct mvae_ctx {
   std::vector<hipEvent_t> event_pool;
   bool timing = false;
   int timing_sel = -1;   // record only this region (-1: all)
+  std::vector<char> marker;  // launch marker kernels around these regions (profiler runs)
   // optimizer state (TF beta1_power / beta2_power are fp32 variables)
   int64_t t1 = 0, t2 = 0;
   float b1p[2] = {0, 0}, b2p[2] = {0, 0};
-  uint64_t rng_counter = 0;
+  uint64_t rng_counter = 0;   // training draws (eps == NULL in mvae_forward / train_step)
+  uint64_t rng_eval = 0;
+  int row_off = 0;            // this rank's first row in the global batch (eps sampling)      // inference draws (predict / reconstruct): a separate stream, so
+                              // evaluation never shifts the training noise sequence
   int phase = 0;  // 0 idle, 1 forward done, 2 metric done, 3 backward done
   std::string err;
 };
@@ -162,10 +168,14 @@ static hipEvent_t take_event(mvae_ctx* c) {
   return e;
 }
 
-// RAII: records a start/stop event pair around one region on the launch stream
+// RAII: records a start/stop event pair around one region on the launch stream; in profiler
+// runs (mvae_timing_marker) it also brackets the region with marker kernels whose grid size
+// (MARKER_GRID + region) names the region in a kernel trace
 struct TimeScope {
-  mvae_ctx* c; int r; hipStream_t st; hipEvent_t a = nullptr;
+  mvae_ctx* c; int r; hipStream_t st; hipEvent_t a = nullptr; bool mk = false;
   TimeScope(mvae_ctx* c_, int r_, hipStream_t st_) : c(c_), r(r_), st(st_) {
+    mk = r < (int)c->marker.size() && c->marker[r];
+    if (mk) (void)launch_marker(r, st);
     if (c->timing && (c->timing_sel < 0 || c->timing_sel == r)) {
       a = take_event(c);
       (void)hipEventRecord(a, st);
@@ -177,6 +187,7 @@ struct TimeScope {
       (void)hipEventRecord(b, st);
       c->pending.push_back({r, a, b});
     }
+    if (mk) (void)launch_marker(r, st);
   }
 };
 
@@ -640,6 +651,26 @@ int mvae_set_step(mvae_ctx* ctx, int64_t t1, int64_t t2) {
   return MVAE_OK;
 }
 
+int mvae_get_rng(mvae_ctx* ctx, uint64_t* train, uint64_t* eval) {
+  if (!ctx || !train || !eval) return MVAE_EINVAL;
+  *train = ctx->rng_counter; *eval = ctx->rng_eval;
+  return MVAE_OK;
+}
+
+int mvae_set_rng(mvae_ctx* ctx, uint64_t train, uint64_t eval) {
+  if (!ctx || (train | eval) & EVAL_STREAM) return MVAE_EINVAL;
+  ctx->rng_counter = train; ctx->rng_eval = eval;
+  return MVAE_OK;
+}
+
+int mvae_set_shard(mvae_ctx* ctx, int64_t row_offset) {
+  if (!ctx) return MVAE_EINVAL;
+  if (row_offset < 0 || row_offset + ctx->B > ctx->cfg.global_batch)
+    return fail(ctx, MVAE_EINVAL, "row_offset outside [0, global_batch - batch]");
+  ctx->row_off = (int)row_offset;
+  return MVAE_OK;
+}
+
 int mvae_sync_params(mvae_ctx* ctx, void* stream) {
   if (!ctx) return MVAE_EINVAL;
   MV_CHECK(launch_split_planes(ctx->theta, ctx->n_all, planes_of(ctx, ctx->theta), (hipStream_t)stream));
@@ -654,7 +685,12 @@ static int run(mvae_ctx* ctx, const GemmDesc& d, hipStream_t st, int r = -1) {
 }
 #define TIMED(name) TimeScope ts_##__LINE__(ctx, region(ctx, name), st)
 
-static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t st) {
+// Encoder pass over the stacked [rot | lock | key] rows. draw: ENC_TRAIN samples eps from the
+// training counter when eps == NULL, ENC_EVAL from the inference counter; ENC_MEAN computes the
+// latent mean/log-sigma heads only (transform: no eps, no z, no column statistics).
+enum { ENC_TRAIN = 0, ENC_EVAL = 1, ENC_MEAN = 2 };
+
+static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t st, int draw = ENC_TRAIN) {
   auto c = ctx;
   {
     TIMED("deinterleave");
@@ -663,18 +699,23 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
                                  c->x32mask, c->x32dyn, st));
   }
   const size_t ne = (size_t)3 * c->B * c->L;
-  {
+  if (draw != ENC_MEAN) {
     TIMED("eps_rng");
     if (eps) {
       MV_CHECK(hipMemcpyAsync(c->eps, eps, ne * sizeof(float), hipMemcpyDeviceToDevice, st));
+    } else if (draw == ENC_TRAIN) {
+      MV_CHECK(launch_normal(c->eps, 3, c->B, c->L, c->cfg.global_batch, c->row_off, c->cfg.seed,
+                             c->rng_counter++, st));
     } else {
-      MV_CHECK(launch_normal(c->eps, ne, c->cfg.seed, c->rng_counter++, st));
+      MV_CHECK(launch_normal(c->eps, 3, c->B, c->L, c->cfg.global_batch, c->row_off, c->cfg.seed,
+                             EVAL_STREAM | c->rng_eval++, st));
     }
   }
   for (size_t i = 0; i < c->fwd_enc.size(); ++i) {
     int rc = run(c, c->fwd_enc[i], st, c->fwd_enc_r[i]);
     if (rc) return rc;
   }
+  if (draw == ENC_MEAN) return MVAE_OK;
   {
     TIMED("latent_fwd");
     MV_CHECK(launch_latent_fwd(c->ms, c->eps, c->z, planes_of(c, c->z), c->B, c->L, c->ldz, st));
@@ -815,7 +856,7 @@ extern "C" int mvae_train_step(mvae_ctx* ctx, const float* x, const float* areas
 extern "C" int mvae_predict(mvae_ctx* ctx, const float* x, const float* eps, float* dist_out, void* stream) {
   if (!ctx || !x || !dist_out) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  int rc = encode(ctx, x, eps, st);
+  int rc = encode(ctx, x, eps, st, ENC_EVAL);
   if (rc) return rc;
   auto c = ctx;
   MV_CHECK(launch_metric(c->z, c->ldz, c->ms, c->rowpart, c->nblk, nullptr, c->colsq, c->B, c->L,
@@ -828,7 +869,7 @@ extern "C" int mvae_predict(mvae_ctx* ctx, const float* x, const float* eps, flo
 extern "C" int mvae_transform(mvae_ctx* ctx, const float* x, float* zmean_out, void* stream) {
   if (!ctx || !x || !zmean_out) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  int rc = encode(ctx, x, nullptr, st);
+  int rc = encode(ctx, x, nullptr, st, ENC_MEAN);
   if (rc) return rc;
   MV_CHECK(launch_copy2d(ctx->ms + (size_t)ctx->B * 2 * ctx->L, 2 * ctx->L, zmean_out, ctx->L,
                          ctx->B, ctx->L, st));
@@ -839,7 +880,7 @@ extern "C" int mvae_transform(mvae_ctx* ctx, const float* x, float* zmean_out, v
 extern "C" int mvae_reconstruct(mvae_ctx* ctx, const float* x, const float* eps, float* y_out, void* stream) {
   if (!ctx || !x || !y_out) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  int rc = encode(ctx, x, eps, st);
+  int rc = encode(ctx, x, eps, st, ENC_EVAL);
   if (rc) return rc;
   if ((rc = run(ctx, ctx->f_d1, st))) return rc;
   if ((rc = run(ctx, ctx->f_d2, st))) return rc;
@@ -857,8 +898,10 @@ extern "C" int mvae_generate(mvae_ctx* ctx, const float* zin, int n, float* y_ou
   auto c = ctx;
   MV_CHECK(launch_copy2d(zin, c->L, c->zgen, c->ldz, n, c->L, st));
   MV_CHECK(launch_split_planes(c->zgen, (size_t)n * c->ldz, planes_of(c, c->zgen), st));
-  GemmDesc d1 = c->f_d1; d1.M = n; d1.A = c->zgen;
-  { const Planes zp = planes_of(c, c->zgen); d1.Ap = zp.p; }
+  // the decoder's first GEMM re-pointed at zgen: fp32 rows and (plane modes) zgen's own plane
+  // images, whose plane stride is B*ldz (z's is 3*B*ldz)
+  GemmDesc d1 = c->f_d1; d1.M = n; d1.A = c->zgen; d1.dynA = nullptr;
+  { const Planes zp = planes_of(c, c->zgen); d1.Ap = zp.p; d1.pA = zp.stride; }
   GemmDesc d2 = c->f_d2; d2.M = n;
   GemmDesc d3 = c->f_out;
   d3.M = n; d3.C = y_out; d3.ldc = c->D; d3.epi = GemmEpi(); d3.epi.mode = EPI_SIGMOID;
@@ -919,6 +962,13 @@ extern "C" int mvae_timing_enable(mvae_ctx* ctx, int on) {
 extern "C" int mvae_timing_select(mvae_ctx* ctx, int region) {
   if (!ctx || region < -1 || region >= (int)ctx->region_names.size()) return MVAE_EINVAL;
   ctx->timing_sel = region;
+  return MVAE_OK;
+}
+
+extern "C" int mvae_timing_marker(mvae_ctx* ctx, int region, int on) {
+  if (!ctx || region < 0 || region >= (int)ctx->region_names.size()) return MVAE_EINVAL;
+  if ((int)ctx->marker.size() < (int)ctx->region_names.size()) ctx->marker.resize(ctx->region_names.size(), 0);
+  ctx->marker[region] = on != 0;
   return MVAE_OK;
 }
 
@@ -984,8 +1034,8 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   hipError_t e = hipMalloc(&A, na * 4);
   if (e == hipSuccess) e = hipMalloc(&Bm, nb * 4);
   if (e == hipSuccess) e = hipMalloc(&Cm, nc * 4);
-  if (e == hipSuccess) e = launch_normal(A, na, 1, 0, st);
-  if (e == hipSuccess) e = launch_normal(Bm, nb, 2, 0, st);
+  if (e == hipSuccess) e = launch_normal(A, 1, 1, (int)na, 1, 0, 1, 0, st);
+  if (e == hipSuccess) e = launch_normal(Bm, 1, 1, (int)nb, 1, 0, 2, 0, st);
   d.A = A; d.B = Bm; d.C = Cm;
   if (e == hipSuccess && np) {
     e = hipMalloc(&planes, (size_t)np * (na + nb) * 2);
@@ -1005,7 +1055,7 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
     d.epi.mode = epi;
     d.epi.act = ACT_TANH;
     if (e == hipSuccess) e = hipMalloc(&aux, (size_t)M * N * 4);
-    if (e == hipSuccess) e = launch_normal(aux, (size_t)M * N, 3, 0, st);
+    if (e == hipSuccess) e = launch_normal(aux, 1, 1, M * N, 1, 0, 3, 0, st);
     if (e == hipSuccess && epi == EPI_BCE) e = hipMalloc(&rowpart, (size_t)M * gemm_bce_nblk(N) * 4);
     d.epi.aux = aux; d.epi.ld_aux = N;
     d.epi.x = aux; d.epi.ldx = N;
@@ -1040,12 +1090,13 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
 
 extern "C" int mvae_make_batch(const unsigned char* locks, const unsigned char* keys, int height,
                                int width, const int* idx, const float* coef, int batch,
-                               float* x_out, void* stream) {
-  if (!locks || !keys || !idx || !coef || !x_out || height <= 0 || width <= 0 || batch <= 0)
+                               float divisor, float* x_out, void* stream) {
+  if (!locks || !keys || !idx || !coef || !x_out || height <= 0 || width <= 0 || batch <= 0 ||
+      !(divisor > 0.f))
     return fail(nullptr, MVAE_EINVAL, "mvae_make_batch: bad argument");
   if ((reinterpret_cast<uintptr_t>(coef) & 15) != 0)
     return fail(nullptr, MVAE_EINVAL, "mvae_make_batch: coef must be 16-byte aligned");
-  hipError_t e = launch_make_batch(locks, keys, height, width, idx, coef, batch, 255.f, x_out,
+  hipError_t e = launch_make_batch(locks, keys, height, width, idx, coef, batch, divisor, x_out,
                                    (hipStream_t)stream);
   if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
   return MVAE_OK;

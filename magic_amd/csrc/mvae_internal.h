@@ -93,7 +93,10 @@ struct Planes {
 // are planes 1-2 (3-plane mode) and the fp32 rows of the blocks in f32dyn_mask written.
 hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int B, int D,
                                int ldx, int f32mask, int f32dyn_mask, hipStream_t st);
-hipError_t launch_normal(float* out, size_t n, uint64_t seed, uint64_t counter, hipStream_t st);
+// N(0,1) into out[slots][B][L]: elements (s*Bg + off + b)*L + l of the counter's global stream
+// (Bg rows per slot over all ranks, this rank's rows starting at off)
+hipError_t launch_normal(float* out, int slots, int B, int L, int Bg, int off, uint64_t seed,
+                         uint64_t counter, hipStream_t st);
 hipError_t launch_latent_fwd(const float* ms, const float* eps, float* z, const Planes& zp, int B,
                              int L, int ldz, hipStream_t st);
 // out[j] for j in [0, ncols): mode 0 = colsq (z_lock^2 | z_key^2), mode 1 = coldot.
@@ -119,6 +122,10 @@ hipError_t launch_split_planes(const float* src, size_t n, const Planes& dst, hi
 hipError_t launch_make_batch(const unsigned char* locks, const unsigned char* keys, int H, int W,
                              const int* idx, const float* coef, int B, float div, float* x,
                              hipStream_t st);
+// empty kernel of MARKER_GRID + region workgroups (64 threads): a region boundary that a
+// rocprofv3 kernel trace shows (counter passes attribute the dispatches between two markers)
+constexpr int MARKER_GRID = 4096;
+hipError_t launch_marker(int region, hipStream_t st);
 hipError_t launch_copy2d(const float* src, int lds, float* dst, int ldd, int rows, int cols,
                          hipStream_t st);
 

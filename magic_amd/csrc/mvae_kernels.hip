@@ -149,10 +149,17 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
   }
 }
 
-__global__ void normal_kernel(float* __restrict__ out, size_t n, uint64_t seed, uint64_t counter) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // one Philox block -> 4 normals
-  if (4 * i >= n) return;
-  uint32_t c[4] = {(uint32_t)i, (uint32_t)(i >> 32), (uint32_t)counter, (uint32_t)(counter >> 32)};
+// One Philox block per thread -> 4 normals at consecutive GLOBAL element indices. With a
+// row-sharded batch the rank's elements of slot s (blockIdx.y) are the contiguous global range
+// [(s*Bg + off)*L, +B*L): a data-parallel rank draws exactly its slice of the eps the single
+// process would draw for the global batch (off = 0, Bg = B: the plain contiguous stream).
+__global__ void normal_kernel(float* __restrict__ out, int B, int L, int Bg, int off, uint64_t seed,
+                              uint64_t counter) {
+  const size_t n = (size_t)B * L;
+  const size_t g0 = ((size_t)blockIdx.y * Bg + off) * L;  // first global element of this slot
+  const size_t q = g0 / 4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // Philox block
+  if (4 * q >= g0 + n) return;
+  uint32_t c[4] = {(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)counter, (uint32_t)(counter >> 32)};
   philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
   const float inv = 2.3283064365386963e-10f;  // 2^-32
   float r[4];
@@ -166,9 +173,12 @@ __global__ void normal_kernel(float* __restrict__ out, size_t n, uint64_t seed, 
     r[2 * j] = rad * co;
     r[2 * j + 1] = rad * s;
   }
+  float* o = out + (size_t)blockIdx.y * n;
 #pragma unroll
-  for (int j = 0; j < 4; ++j)
-    if (4 * i + j < n) out[4 * i + j] = r[j];
+  for (int j = 0; j < 4; ++j) {
+    const size_t e = 4 * q + j;
+    if (e >= g0 && e < g0 + n) o[e - g0] = r[j];
+  }
 }
 
 // ---------------------------------------------------------------- reparameterisation
@@ -452,6 +462,8 @@ __global__ void make_batch_kernel(const unsigned char* __restrict__ locks,
 
 inline unsigned nblocks(size_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
+__global__ void mvae_region_marker() {}
+
 }  // namespace
 
 hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int B, int D,
@@ -472,8 +484,13 @@ hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int*
   return hipGetLastError();
 }
 
-hipError_t launch_normal(float* out, size_t n, uint64_t seed, uint64_t counter, hipStream_t st) {
-  hipLaunchKernelGGL(normal_kernel, dim3(nblocks((n + 3) / 4, 256)), dim3(256), 0, st, out, n, seed, counter);
+hipError_t launch_normal(float* out, int slots, int B, int L, int Bg, int off, uint64_t seed,
+                         uint64_t counter, hipStream_t st) {
+  const size_t n = (size_t)B * L;
+  if (n == 0 || slots <= 0) return hipSuccess;
+  // Philox blocks touched by one slot's range: at most n/4 + 2
+  dim3 g(nblocks(n / 4 + 2, 256), slots);
+  hipLaunchKernelGGL(normal_kernel, g, dim3(256), 0, st, out, B, L, Bg, off, seed, counter);
   return hipGetLastError();
 }
 
@@ -538,6 +555,11 @@ hipError_t launch_make_batch(const unsigned char* locks, const unsigned char* ke
   dim3 g(nblocks((size_t)H * W, 256), B);
   hipLaunchKernelGGL(make_batch_kernel, g, dim3(256), 0, st, locks, keys, H, W, idx,
                      reinterpret_cast<const float4*>(coef), div, x);
+  return hipGetLastError();
+}
+
+hipError_t launch_marker(int region, hipStream_t st) {
+  hipLaunchKernelGGL(mvae_region_marker, dim3(MARKER_GRID + region), dim3(64), 0, st);
   return hipGetLastError();
 }
 

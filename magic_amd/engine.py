@@ -158,6 +158,19 @@ class Engine:
     def set_step(self, t1: int, t2: int):
         self._check(self.lib.mvae_set_step(self.ctx, t1, t2))
 
+    def set_shard(self, row_offset: int):
+        """This rank's first row in the global batch (the internal eps sampler draws the
+        rank's slice of the global stream)."""
+        self._check(self.lib.mvae_set_shard(self.ctx, row_offset))
+
+    def get_rng(self):
+        a, b = C.c_uint64(), C.c_uint64()
+        self._check(self.lib.mvae_get_rng(self.ctx, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
+    def set_rng(self, train: int, eval_: int):
+        self._check(self.lib.mvae_set_rng(self.ctx, train, eval_))
+
     # ------------------------------------------------------------------ step phases
     def _xin(self, x):
         if x.shape != (self.cfg.batch, 3 * self.cfg.D):
@@ -240,6 +253,14 @@ class Engine:
                      for i in range(self.lib.mvae_timing_regions(self.ctx))]
             r = names.index(name)
         self._check(self.lib.mvae_timing_select(self.ctx, r))
+
+    def timing_names(self):
+        return [self.lib.mvae_timing_name(self.ctx, i).decode()
+                for i in range(self.lib.mvae_timing_regions(self.ctx))]
+
+    def timing_marker(self, name: str, on: bool = True):
+        """Bracket region ``name`` with marker kernels (rocprofv3 counter attribution)."""
+        self._check(self.lib.mvae_timing_marker(self.ctx, self.timing_names().index(name), int(on)))
 
     def timing_reset(self):
         self._check(self.lib.mvae_timing_reset(self.ctx))

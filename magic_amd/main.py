@@ -1,7 +1,23 @@
-"""Training driver — mirror of ``11a/main.py:42-133`` (and the 8c variant ``8c/main.py:33-94``)
+"""Training driver — mirror of ``11a/main.py:42-133`` and of the 8c variant ``8c/main.py:33-94``
 on the HIP step. No HTTP "poor man's tensorboard" (``11a/utils.py:256-266``) and no plots.
 
   python -m magic_amd.main --preset 8c --image-size 100 --batch 4096 --epochs 2
+
+The two reference drivers differ in four ways, all reproduced (``driver=``):
+
+  =============  ===========================================  ================================
+                 11a (``11a/main.py``)                         8c (``8c/main.py``)
+  =============  ===========================================  ================================
+  eval cadence   ``epoch % 10 == 0 and i == 3`` (:93)          ``i % 24 == 0`` (:66)
+  eval fetch     images + labels of ONE dequeue (:94)          two dequeues: images and labels
+                                                               do not match (:67-68)
+  predictions    ``1. / predictions`` (:100)                   as returned (:69)
+  epoch log      average cost and average loss (:121-126)      average cost every 5th epoch
+                                                               (:84,87-89)
+  =============  ===========================================  ================================
+
+Both raise ``TrainingException("Got cost=nan")`` when ``partial_fit`` returns a NaN cost
+(11a :77-78, 8c :51-52) and swallow ``KeyboardInterrupt`` (11a :130-131, 8c :91-92).
 """
 from __future__ import annotations
 
@@ -14,22 +30,38 @@ import numpy as np
 from . import overlap_input
 from .config import preset
 from .constants import FLAGS
-from .vae import TangoEncoder
 
 
 class TrainingException(Exception):
-    """``11a/excps.py:3-4``."""
+    """``11a/excps.py:3-4`` (``8c/main.py:29-30``)."""
 
 
-def train(vae: TangoEncoder, batches, n_samples: int, training_epochs: int = 60,
-          eval_every_epochs: int = 10, eval_step: int = 3, paired_eval: bool = True,
-          log=print):
-    """``11a/main.py:42-133``: per-step ``partial_fit``, NaN guard, overlap-MSE eval at
-    (epoch % 10 == 0, i == 3) on a fresh batch, epoch averages. With
-    ``paired_eval=False`` the eval images and labels come from two different draws, as
-    ``8c/main.py:44-45,67-68`` fetched them (reproduces the README's MSE setting)."""
+DRIVERS = {
+    # eval predicate (epoch, i), paired eval fetch, invert predictions, log both averages
+    "11a": dict(eval_at=lambda epoch, i: epoch % 10 == 0 and i == 3, paired=True, invert=True),
+    "8c": dict(eval_at=lambda epoch, i: i % 24 == 0, paired=False, invert=False),
+}
+
+
+def _host(a):
+    return a.detach().cpu().numpy() if hasattr(a, "detach") else np.asarray(a)
+
+
+def train(vae, batches, n_samples: int, training_epochs: int = 60, driver: str = "11a",
+          invert=None, paired_eval=None, eval_at=None, display_step: int = 5, log=print):
+    """Run the reference training loop. ``batches`` yields (images, labels) like the
+    reference's ``sess.run([images_batch, labels_batch])``.
+
+    invert: ``1/pred`` before the MSE; default: the driver's choice for a reciprocal model
+    (11a inverts because its distance is the reciprocal, ``11a/vae.py:307,309``; a model
+    without the reciprocal is never inverted). Returns (vae, history): history holds
+    ("mse", epoch, i, mse) and ("epoch", epoch, avg_cost, avg_loss) records."""
+    d = DRIVERS[driver]
+    eval_at = eval_at or d["eval_at"]
+    paired = d["paired"] if paired_eval is None else paired_eval
+    if invert is None:
+        invert = d["invert"] and bool(getattr(vae.config, "reciprocal", True))
     batch_size = vae.batch_size
-    invert = vae.config.reciprocal
     history = []
     try:
         for epoch in range(training_epochs):
@@ -42,21 +74,24 @@ def train(vae: TangoEncoder, batches, n_samples: int, training_epochs: int = 60,
                 cost, training_loss = out[0], out[1]
                 if np.isnan(cost):
                     raise TrainingException("Got cost=nan")
-                if epoch % eval_every_epochs == 0 and i == eval_step:
+                if eval_at(epoch, i):
                     test_x, test_a = next(batches)
-                    if not paired_eval:
-                        _, test_a = next(batches)
-                    pred = vae.get_predictions(test_x, test_a)
+                    if not paired:
+                        _, test_a = next(batches)  # 8c: a second dequeue for the labels
+                    pred = np.asarray(vae.get_predictions(test_x, test_a), np.float64)
                     if invert:
-                        pred = 1.0 / pred  # 11a/main.py:100
-                    a = test_a.cpu().numpy() if hasattr(test_a, "cpu") else np.asarray(test_a)
-                    mse = float(((np.asarray(pred, np.float64) - a) ** 2).mean())
+                        pred = 1.0 / pred
+                    mse = float(((pred - _host(test_a).astype(np.float64)) ** 2).mean())
                     log(f"mse: {mse}")
-                    history.append(("mse", epoch, mse))
+                    history.append(("mse", epoch, i, mse))
                 avg_cost += cost / n_samples * batch_size
                 avg_loss += training_loss / n_samples * batch_size
-            log(f"Epoch: {epoch}".ljust(20) + f"Average cost: {int(avg_cost)}".ljust(35)
-                + f"Average loss: {int(avg_loss)}".ljust(35))
+            if driver == "8c":
+                if epoch % display_step == 0:
+                    log(f"Epoch: {epoch + 1:04d} cost= {avg_cost:.9f}")
+            else:
+                log(f"Epoch: {epoch}".ljust(20) + f"Average cost: {int(avg_cost)}".ljust(35)
+                    + f"Average loss: {int(avg_loss)}".ljust(35))
             history.append(("epoch", epoch, avg_cost, avg_loss))
     except KeyboardInterrupt:
         pass
@@ -64,22 +99,26 @@ def train(vae: TangoEncoder, batches, n_samples: int, training_epochs: int = 60,
 
 
 def main(argv=None):
+    from .vae import TangoEncoder
     ap = argparse.ArgumentParser()
     ap.add_argument("--preset", default="11a")
     ap.add_argument("--image-size", type=int, default=FLAGS.IMAGE_SIZE)
     ap.add_argument("--batch", type=int, default=0)
     ap.add_argument("--epochs", type=int, default=3)
-    ap.add_argument("--data", default=None, help="dir/.zip of {N}_L.png/{N}_K.png (default synthetic)")
+    ap.add_argument("--data", default=None, help="dir/.zip of {N}_L.png/{N}_K.png or a packed .npz "
+                                                 "(default: synthetic shapes)")
     ap.add_argument("--samples-per-epoch", type=int, default=FLAGS.NUM_EXAMPLES_PER_EPOCH_FOR_TRAIN)
-    ap.add_argument("--unpaired-eval", action="store_true", help="8c driver semantics")
+    ap.add_argument("--driver", choices=sorted(DRIVERS), default=None,
+                    help="reference driver semantics (default: 8c for the 8c-family presets)")
     args = ap.parse_args(argv)
     cfg = preset(args.preset, image_size=args.image_size, batch=args.batch or None)
-    vae = TangoEncoder(None, config=cfg, compat="8c" if args.preset in ("8c", "8d", "8e", "8f") else "11a")
+    eight_c = args.preset in ("8c", "8d", "8e", "8f")
+    driver = args.driver or ("8c" if eight_c else "11a")
+    vae = TangoEncoder(None, config=cfg, compat="8c" if eight_c else "11a")
     batches = overlap_input.inputs(normalize=True, reshape=True, rotation=True, batch_size=cfg.batch,
                                    image_size=cfg.image_size, data_dir=args.data)
     t0 = time.time()
-    train(vae, batches, max(args.samples_per_epoch, cfg.batch), args.epochs,
-          paired_eval=not args.unpaired_eval)
+    train(vae, batches, max(args.samples_per_epoch, cfg.batch), args.epochs, driver=driver)
     print(f"done in {time.time() - t0:.1f}s", file=sys.stderr)
     vae.close()
 

@@ -43,9 +43,10 @@ def rotation_coefficients(angles, height: int, width: int) -> np.ndarray:
 
 
 def make_batch(locks: torch.Tensor, keys: torch.Tensor, idx: torch.Tensor, coef: torch.Tensor,
-               out: Optional[torch.Tensor] = None) -> torch.Tensor:
+               out: Optional[torch.Tensor] = None, normalize: bool = True) -> torch.Tensor:
     """HIP batch producer (``mvae_make_batch``): uint8 device tables [n, H, W], idx int32 [B],
-    coef float32 [B, 4] -> X float32 [B, H*W*3] = per pixel (lock, rotated lock, key) / 255."""
+    coef float32 [B, 4] -> X float32 [B, H*W*3] = per pixel (lock, rotated lock, key) / 255
+    (``normalize=False``: the raw 0..255 values, ``11a/overlap_input.py:113-115``)."""
     from . import _lib
     lib = _lib.load()
     n, h, w = locks.shape
@@ -55,7 +56,8 @@ def make_batch(locks: torch.Tensor, keys: torch.Tensor, idx: torch.Tensor, coef:
             raise ValueError("make_batch: device tensors (uint8 tables, int32 idx, float32 coef) expected")
     out = out if out is not None else torch.empty(B, 3 * h * w, device=locks.device)
     rc = lib.mvae_make_batch(locks.data_ptr(), keys.data_ptr(), h, w, idx.data_ptr(), coef.data_ptr(),
-                             B, out.data_ptr(), torch.cuda.current_stream(locks.device).cuda_stream)
+                             B, 255.0 if normalize else 1.0, out.data_ptr(),
+                             torch.cuda.current_stream(locks.device).cuda_stream)
     _lib.check(lib, None, rc)
     return out
 
@@ -171,10 +173,10 @@ class BatchStream:
     per-batch assembly runs in the HIP batch producer (``mvae_make_batch``)."""
 
     def __init__(self, batch: int, image_size: int, source: Optional[PairSource] = None,
-                 normalize: bool = True, seed: int = 1, device="cuda", synthetic_pool: int = 960):
-        if not normalize:
-            raise ValueError("the HIP batch producer emits normalised pixels (/255)")
+                 normalize: bool = True, seed: int = 1, device="cuda", synthetic_pool: int = 960,
+                 reshape: bool = True, fp16: bool = False):
         self.batch, self.size = batch, image_size
+        self.normalize, self.reshape, self.fp16 = normalize, reshape, fp16
         self.device = torch.device(device)
         self.rng = np.random.default_rng(seed)
         if source is None:  # synthetic pool of pairs, re-rotated every draw
@@ -215,14 +217,21 @@ class BatchStream:
         ang = self.rng.uniform(0.0, 2 * math.pi, self.batch)
         coef = torch.from_numpy(rotation_coefficients(ang, self.size, self.size)).to(self.device)
         idx_t = torch.from_numpy(idx.astype(np.int32)).to(self.device)
-        x = make_batch(self.locks, self.keys, idx_t, coef)
-        return x, self.areas[idx_t.long()]
+        x = make_batch(self.locks, self.keys, idx_t, coef, normalize=self.normalize)
+        a = self.areas[idx_t.long()]
+        if not self.reshape:  # [B, H, W, 3] (11a/overlap_input.py:117-119 not applied)
+            x = x.view(self.batch, self.size, self.size, 3)
+        if self.fp16:  # FLAGS.USE_FP16 casts images and labels (11a/overlap_input.py:109-111)
+            x, a = x.half(), a.half()
+        return x, a
 
 
 def inputs(normalize: bool = False, reshape: bool = False, rotation: bool = False,
            batch_size: Optional[int] = None, image_size: Optional[int] = None,
            data_dir: Optional[str] = None, device="cuda", seed: int = 1) -> BatchStream:
-    """``11a/overlap_input.py:76``. ``reshape`` is implied (the stream yields [B, 3D])."""
+    """``11a/overlap_input.py:76-122``: images [B, H*W*3] (``reshape=True``) or [B, H, W, 3],
+    divided by 255 when ``normalize``, cast to float16 with labels when ``FLAGS.USE_FP16``;
+    ``rotation=False`` raises as in the reference (``:95-96``)."""
     if not rotation:
         raise ValueError("Rotation has to be True.")
     size = image_size or FLAGS.IMAGE_SIZE
@@ -232,4 +241,5 @@ def inputs(normalize: bool = False, reshape: bool = False, rotation: bool = Fals
     if d:
         lim = FLAGS.NUM_EXAMPLES_TO_LOAD_INTO_QUEUE
         src = PairSource.from_packed(d, limit=lim) if d.endswith(".npz") else PairSource(d, limit=lim)
-    return BatchStream(bs, size, src, normalize=normalize, seed=seed, device=device)
+    return BatchStream(bs, size, src, normalize=normalize, seed=seed, device=device, reshape=reshape,
+                       fp16=bool(getattr(FLAGS, "USE_FP16", False)))

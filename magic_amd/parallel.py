@@ -42,6 +42,11 @@ class DataParallelStep:
         if engine.cfg.gbatch != engine.cfg.batch * self.world:
             raise ValueError(f"engine global_batch {engine.cfg.gbatch} != batch {engine.cfg.batch} "
                              f"x world {self.world}")
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        if hasattr(engine, "set_shard"):
+            # the internal eps sampler draws this rank's rows of the global batch's stream,
+            # so a sharded step without explicit eps equals the single-process step too
+            engine.set_shard(self.rank * engine.cfg.batch)
 
     def _ar(self, t):
         if self.world > 1:

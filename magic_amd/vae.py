@@ -38,7 +38,8 @@ def _default_config() -> MVAEConfig:
 
 class TangoEncoder(object):
     def __init__(self, sess=None, config: Optional[MVAEConfig] = None, device: int = 0,
-                 compat: str = "11a", init_seed: int = 0, data_parallel=None):
+                 compat: str = "11a", init_seed: int = 0, data_parallel=None,
+                 tf_nonfinite: bool = True):
         self.sess = sess  # kept for signature compatibility (11a/vae.py:22)
         cfg = config or _default_config()
         self.config = cfg
@@ -59,6 +60,15 @@ class TangoEncoder(object):
             self._dp = DataParallelStep(self.engine, group=None if data_parallel is True else data_parallel)
         self._losses = torch.empty(5, device=self.engine.dev)
         self._dist = torch.empty(cfg.batch, device=self.engine.dev)
+        # Non-finite cost (e.g. BCE saturation: the sigmoid rounds to 1.0 on a 0 pixel, so
+        # log(pow(1-y, 1-x)) = log(0) and R = +inf with no epsilon, 11a/vae.py:266-267).
+        # TF's gradient of that pow/log chain is NaN (inf * 0), so after such a step every
+        # reference parameter is NaN and the NEXT partial_fit returns cost = nan, which the
+        # driver's guard turns into TrainingException (11a/main.py:77-78). This build's
+        # gradient dU = (y - x)/B stays finite; tf_nonfinite=True reproduces the reference's
+        # observable behaviour by reporting NaN losses from the step after a non-finite cost.
+        self.tf_nonfinite = tf_nonfinite
+        self._poisoned = False
 
     # ----------------------------------------------------------------- helpers
     def _dev(self, a, shape):
@@ -79,6 +89,11 @@ class TangoEncoder(object):
         x = self._x(X)
         a = self._dev(overlap_areas, (self.batch_size,))
         e = None if eps is None else self._dev(eps, (3, self.batch_size, self.latent_dimensions))
+        if self._poisoned:
+            nan = float("nan")
+            if self.compat == "8c":
+                return nan, nan, nan, nan, nan
+            return nan, nan, nan, nan, nan, np.full(self.batch_size, np.nan, np.float32)
         if self._dp is None:
             self.engine.train_step(x, a, e, losses_out=self._losses, dist_out=self._dist)
             losses = self._losses
@@ -87,6 +102,8 @@ class TangoEncoder(object):
             self._dist.copy_(self.engine.dist)
         l = losses.cpu().numpy().astype(np.float64)
         cost, training_loss, rec_loss, lat_loss, def_loss = (float(v) for v in l[:5])
+        if self.tf_nonfinite and not np.isfinite(cost):
+            self._poisoned = True
         if self.compat == "8c":
             return cost, training_loss, rec_loss, lat_loss, def_loss
         return cost, training_loss, rec_loss, lat_loss, def_loss, self._dist.cpu().numpy()
@@ -120,6 +137,7 @@ class TangoEncoder(object):
                 out[f"{tag}/{k}"] = v.detach().cpu().clone()
         t1, t2 = self.engine.get_step()
         out["step"] = torch.tensor([t1, t2])
+        out["rng"] = torch.tensor(list(self.engine.get_rng()), dtype=torch.int64)
         return out
 
     def load_state_dict(self, sd):
@@ -131,6 +149,8 @@ class TangoEncoder(object):
                 v.copy_(sd[f"{tag}/{k}"].to(v.device))
         t1, t2 = (int(x) for x in sd["step"])
         self.engine.set_step(t1, t2)
+        if "rng" in sd:
+            self.engine.set_rng(*(int(x) for x in sd["rng"]))
         self.engine.sync_params()
         torch.cuda.synchronize(self.engine.dev)
 

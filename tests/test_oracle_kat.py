@@ -99,3 +99,27 @@ def test_statistical_step0_magnitudes(L, logged_deform):
     assert abs(r - 27734.2) / 27734.2 < 0.01, r
     assert abs(d - logged_deform) / logged_deform < 0.25, d
     assert 0 < k < 20 * (L / 20), k
+
+
+def test_kat_bce_saturation_forward_inf_gradient_finite():
+    """BCE with no epsilon (``11a/vae.py:266-267``): once the sigmoid rounds to 1.0 on a 0
+    pixel, log(pow(1-y, 1-x)) = log(0) and R = +inf (np.isnan(inf) is False, so the
+    reference's guard ``11a/main.py:77`` lets the step through). The restatement keeps that
+    forward value and the analytic gradient dU = (y - x)/B, which stays finite (TF's pow/log
+    chain rule gives NaN there: DESIGN.md §2, "BCE saturation")."""
+    cfg = cfg8c(image=4, enc=(8, 8), L=3)
+    B = 3
+    P = O.init_params(cfg, seed=0, dtype=np.float64)
+    P["dec_out_mean_b"][0] = 60.0          # pixel 0: u >= 60 - |d2 Vo| -> y == 1.0 exactly
+    X = np.zeros((B, 3 * cfg.D))           # all-zero target at pixel 0
+    X[:, 3 * 5] = 1.0
+    eps = np.random.default_rng(2).standard_normal((3, B, cfg.latent))
+    c = O.forward(P, X, eps, cfg)
+    assert np.all(c["y"][:, 0] == 1.0)
+    assert np.all(np.isposinf(c["R"]))
+    O.metric(c, np.full(B, 500.0), cfg, B)
+    losses = O.loss_sums(c, B)
+    assert np.isposinf(losses[0]) and np.isposinf(losses[2]) and np.isfinite(losses[1])
+    g1, g2 = O.backward(c, cfg, B)
+    assert all(np.all(np.isfinite(v)) for v in list(g1.values()) + list(g2.values()))
+    np.testing.assert_allclose(g1["dec_out_mean_b"][0], 1.0, rtol=0)  # sum_b (1 - 0)/B
