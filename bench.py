@@ -3,39 +3,91 @@
 reference ``11a/vae.py:385-411``) on MI355X through libmvae's HIP kernels.
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config C2]
-  N>1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+``--gpus N`` with N > 1 and no torchrun environment starts N local ranks itself
+(``torch.distributed.run``, one process per GPU, RCCL); under torchrun it is one of them.
 
 A step = one pass of the hot path over one batch of synthetic 100x100 shape pairs already
 resident in HBM: de-interleave, eps sampling, 3 encoder passes, decoder, five-loss head,
-both gradients, (N>1: RCCL all-reduces), both Adam updates. Weak scaling: the per-GPU batch
-is fixed; ``value`` = pairs processed by ALL ranks / max-over-ranks wall time.
+both gradients, (N > 1: RCCL all-reduces), both Adam updates. Weak scaling: the per-GPU
+batch is fixed; ``value`` = pairs processed by ALL ranks / max-over-ranks wall time.
 
-Rank 0 prints ONE JSON line. Extra diagnostics (per-region HIP-event timings) go to stderr.
+Rank 0 prints ONE JSON line; per-region HIP-event timings go to stderr. Besides the
+contract's fields the line carries:
+  roofline       the dominant GEMM: algorithmic FLOPs (2*M*N*K once) / its
+                 mean HIP-event duration in the timed loop, against the dense MFMA peak of
+                 the arithmetic it runs on; f32x (fp32-accurate bf16 plane split) adds
+                 mfma_pipe_frac = plane-pair bf16 work / time / bf16 peak. traffic = HBM
+                 bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes run by this
+                 process (child runs, marker-bracketed region, MI355X_MICROARCH.md §HBM).
+  loss_roofline  the HBM-bound kernels (de-interleave, sampler, latent head, metric, Adam)
+                 and the BCE epilogue: algorithmic bytes per launch / time vs 8 TB/s.
+  cpu_baseline   the CPU restatement (oracle, numpy fp32 + BLAS) on this host: the
+                 GPU-batch workload with all threads, C1 (B=64) with all threads and with 1
+                 thread, and the in-run parity of the GPU C1 step against it.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
+import signal
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
-import torch
-import torch.distributed as dist
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
-
-from magic_amd import _lib  # noqa: E402
-from magic_amd.config import baseline_config  # noqa: E402
 
 METRIC = "shape-pairs/sec/GPU (train step) + overlap-MSE, 100×100 pairs, 1/2/4/8 GPUs"
 F32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (exact fp32)
 BF16_MFMA_PEAK_TFLOPS = 2500.0   # dense
 HBM_PEAK_GBS = 8000.0
+PMC_REGIONS_BW = ("deinterleave", "latent_bwd", "adam")
 
 
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="C2", help="BASELINE config id (C2 fp32 B=4096 default)")
+    ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch")
+    ap.add_argument("--precision", default="", help="override GEMM arithmetic: f32 | f32x | bf16")
+    ap.add_argument("--cpu-seconds", type=float, default=3.0, help="per CPU-baseline timing leg")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="disable per-region HIP events")
+    ap.add_argument("--region-steps", type=int, default=10,
+                    help="extra steps with every region timed (per-kernel table, dominant GEMM)")
+    ap.add_argument("--pmc", default="auto", choices=["auto", "off"],
+                    help="rocprofv3 FETCH_SIZE/WRITE_SIZE child passes for roofline.traffic")
+    ap.add_argument("--pmc-child", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="CPU rehearsal of the launcher / data-parallel / timing / JSON path "
+                         "(gloo, a stand-in engine; no GPU, no kernels, not a measurement)")
+    return ap.parse_args(argv)
+
+
+# ------------------------------------------------------------------------ launcher
+def self_launch(args, argv) -> int:
+    """N > 1 without a torchrun environment: start N local ranks (one process per GPU) as a
+    child torch.distributed.run before this process touches the GPU, and exit with its code."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__), *argv]
+    return subprocess.call(cmd)
+
+
+# ------------------------------------------------------------------------ work models
 def region_flops(cfg, name: str) -> float:
     """Algorithmic FLOPs of one launch of a timed GEMM region (2*M*N*K, K = fan-in)."""
     B, D, L = cfg.batch, cfg.D, cfg.latent
@@ -62,99 +114,385 @@ def region_flops(cfg, name: str) -> float:
     return table.get(name, 0.0)
 
 
-def cpu_baseline(cfg, seconds: float):
-    """The oracle (CPU restatement, numpy fp32 + BLAS) timed on this host on a bounded
-    sample of the same workload: C2 widths, a 256-pair batch, >= 2 steps, ~`seconds`."""
-    from oracle import mvae_oracle as O
+def plane_pairs(cfg, name: str, exact_pixels: bool) -> int:
+    """bf16 MFMA products per fp32 product in the f32x split: 6 plane pairs (i + j < 3), 3 when
+    the A operand is the exact binary pixel operand (layer 0)."""
+    return 3 if name in ("enc_fwd_0", "enc_bwd_w_0") and exact_pixels else 6
+
+
+def region_bytes(cfg, name: str) -> float:
+    """Algorithmic HBM bytes per launch of a bandwidth-bound region: every operand read once and
+    every output written once at its stored width (fp32 = 4 B; bf16 plane images = 2 B per plane,
+    np planes per value: 0 in f32 mode, 1 bf16, 3 f32x). Counts follow the kernels' inputs and
+    outputs in magic_amd/csrc/mvae_kernels.hip; the per-pair latent-head figure of SURVEY.md §8d
+    (~80 L B/pair, the minimum of a fully fused head) is reported beside them."""
+    B, D, L = cfg.batch, cfg.D, cfg.latent
+    np_ = {"f32": 0, "bf16": 1, "f32x": 3}[cfg.precision]
+    BL = B * L
+    if name == "deinterleave":  # fp32 X read; bf16 plane 0 of 3 blocks (plane modes) or fp32 xs
+        return B * D * (12.0 + (6.0 if np_ else 12.0))
+    if name == "eps_rng":
+        return 3 * BL * 4.0
+    if name == "latent_fwd":    # ms (mu, s) + eps in; z + its planes out
+        return 3 * BL * (8.0 + 4.0 + 4.0 + 2.0 * np_)
+    if name == "colsq":
+        return 2 * BL * 4.0
+    if name == "metric_loss":   # z (3 blocks) + lock mu, s + areas/rowpart in; 4 row values out
+        return 3 * BL * 4.0 + 2 * BL * 4.0 + B * 4.0 * 6
+    if name == "coldot":
+        return 2 * BL * 4.0 + B * 4.0
+    if name == "latent_bwd":    # z (3 blocks), mu/s (3 blocks), eps (3), dz_dec in; dhead (4 rows x 2L) out
+        return BL * (12.0 + 24.0 + 12.0 + 4.0) + 4 * BL * 2 * (4.0 + 2.0 * np_)
+    return 0.0
+
+
+def adam_bytes(n_all: int, n_enc: int, np_: int) -> float:
+    """Fused dual Adam: theta, g1, m1, v1 (+ g2, m2, v2 on the encoder slice) in, theta, m1, v1
+    (+ m2, v2) and the parameter planes out."""
+    return n_all * (16.0 + 12.0 + 2.0 * np_) + n_enc * (12.0 + 8.0)
+
+
+# ------------------------------------------------------------------------ PMC passes
+def _csv_rows(d, suffix):
+    import csv
+    import glob
+    out = []
+    for p in glob.glob(os.path.join(d, "**", f"*{suffix}"), recursive=True):
+        with open(p) as f:
+            out.extend(csv.DictReader(f))
+    return out
+
+
+def _region_counter(d, counter, region_ids):
+    """Mean per launch of `counter` (summed over the dispatches between each pair of marker
+    kernels of a region) for every region id, from one rocprofv3 output directory."""
+    vals = {}
+    for r in _csv_rows(d, "counter_collection.csv"):
+        if r.get("Counter_Name") == counter:
+            k = int(r["Dispatch_Id"])
+            vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
+    trace = sorted(_csv_rows(d, "kernel_trace.csv"), key=lambda r: int(r["Dispatch_Id"]))
+    from magic_amd._lib import MARKER_GRID
+
+    def wgs(r):
+        g = int(r.get("Grid_Size_X") or r.get("Grid_Size") or 0)
+        return g // max(1, int(r.get("Workgroup_Size_X") or r.get("Workgroup_Size") or 1))
+    out = {}
+    for rid in region_ids:
+        sums, open_ = [], None
+        for r in trace:
+            if "mvae_region_marker" in r["Kernel_Name"]:
+                if wgs(r) != MARKER_GRID + rid:
+                    continue
+                if open_ is None:
+                    open_ = (int(r["Dispatch_Id"]), r.get("Queue_Id"))
+                else:
+                    lo, q = open_
+                    hi = int(r["Dispatch_Id"])
+                    ids = [int(x["Dispatch_Id"]) for x in trace
+                           if lo < int(x["Dispatch_Id"]) < hi and x.get("Queue_Id") == q
+                           and "mvae_region_marker" not in x["Kernel_Name"]]
+                    sums.append(sum(vals.get(i, 0.0) for i in ids))
+                    open_ = None
+        if sums:
+            out[rid] = sum(sums) / len(sums)
+    return out
+
+
+def pmc_traffic(args, names, regions_all):
+    """HBM bytes per launch of each region in `names`: two rocprofv3 child runs of this bench
+    (FETCH_SIZE and WRITE_SIZE cannot share a pass), markers around the regions; FETCH_SIZE x2
+    (gfx950 reports half of a wide streaming read) and KB -> B."""
+    exe = shutil.which("rocprofv3")
+    if not exe:
+        return None, "rocprofv3 not on PATH"
+    ids = {n: regions_all.index(n) for n in names if n in regions_all}
+    base = os.path.join(HERE, "gpurun_out") if os.path.isdir(os.path.join(HERE, "gpurun_out")) \
+        else tempfile.gettempdir()
+    root = tempfile.mkdtemp(prefix="bench_pmc_", dir=base)
+    child = [sys.executable, os.path.abspath(__file__), "--pmc-child", ",".join(str(r) for r in ids.values()),
+             "--config", args.config, "--steps", "2", "--warmup", "1"]
+    if args.batch:
+        child += ["--batch", str(args.batch)]
+    if args.precision:
+        child += ["--precision", args.precision]
+    res = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        d = os.path.join(root, counter.lower())
+        cmd = [exe, "--pmc", counter, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run",
+               "--", *child]
+        env = dict(os.environ, TMPDIR="/tmp")
+        with open(os.path.join(root, counter.lower() + ".log"), "w") as log:
+            p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT,
+                                 start_new_session=True)
+            try:
+                rc = p.wait(timeout=150)
+            except subprocess.TimeoutExpired:
+                os.killpg(p.pid, signal.SIGKILL)
+                p.wait()
+                return None, f"{counter} pass timed out"
+        if rc != 0:
+            return None, f"{counter} pass rc={rc} (log {root})"
+        res[counter] = _region_counter(d, counter, list(ids.values()))
+    out = {}
+    for n, rid in ids.items():
+        f, w = res["FETCH_SIZE"].get(rid), res["WRITE_SIZE"].get(rid)
+        if f is not None and w is not None:
+            out[n] = {"hbm_bytes": round(f * 1024 * 2 + w * 1024),
+                      "fetch_bytes": round(f * 1024 * 2), "write_bytes": round(w * 1024)}
+    return out, f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child passes, marker-bracketed ({root})"
+
+
+# ------------------------------------------------------------------------ CPU baseline
+def _cpu_model():
     try:
-        from threadpoolctl import threadpool_info
-        cores = max([i.get("num_threads", 1) for i in threadpool_info() if i.get("user_api") == "blas"] or [1])
-    except Exception:
-        cores = os.cpu_count() or 1
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(cfg, dev, seconds: float):
+    """The oracle (CPU restatement of the reference maths, numpy fp32 + BLAS) on this host:
+    (1) parity: one C1-shaped step (B = 64, this run's GEMM arithmetic) on the GPU and on the
+    CPU from the same seeded batch, eps and parameters; (2) timings: the GPU-batch workload
+    with all BLAS threads (`value`), C1 with all threads and with 1 thread."""
+    import torch
+    from threadpoolctl import threadpool_info, threadpool_limits
+
+    from magic_amd import _lib
+    from magic_amd.engine import Engine
+    from magic_amd.overlap_input import synthetic_batch
+    from oracle import mvae_oracle as O
+
     oc = O.OracleConfig(image_size=cfg.image_size, enc=tuple(cfg.enc), dec=tuple(cfg.dec),
                         latent=cfg.latent, act=cfg.act, deform_weight=cfg.deform_weight,
                         metric=cfg.metric, reciprocal=cfg.reciprocal, lr=tuple(cfg.lr))
-    Bc = 256
-    rng = np.random.default_rng(1)
-    X = (rng.random((Bc, 3 * cfg.D)) < 0.08).astype(np.float32)
-    areas = rng.integers(296, 6427, Bc).astype(np.float32)
-    P = O.init_params(oc, seed=0, dtype=np.float32)
-    st = O.adam_init(oc, P)
-    eps = rng.standard_normal((3, Bc, cfg.latent)).astype(np.float32)
-    O.train_step(P, st, X, areas, eps, oc, dtype=np.float32)  # warm-up
-    t0 = time.perf_counter()
-    n = 0
-    while n < 2 or time.perf_counter() - t0 < seconds:
-        _, _, P, st, _ = O.train_step(P, st, X, areas, eps, oc, dtype=np.float32)
-        n += 1
-    dt = time.perf_counter() - t0
-    return {"value": round(n * Bc / dt, 2), "unit": "shape-pairs/s", "cores": int(cores),
-            "kind": "port",
-            "sample": f"oracle/mvae_oracle.py train_step, numpy float32 + OpenBLAS, {n} steps x "
-                      f"{Bc} pairs of the {cfg.image_size}x{cfg.image_size} {len(cfg.enc)}x{cfg.enc[0]} "
-                      f"L={cfg.latent} step, {dt:.1f} s"}
+    B1 = 64
+    c1 = cfg.replace(batch=B1, global_batch=B1)
+    x1, a1 = synthetic_batch(B1, cfg.image_size, seed=4242, device=dev)
+    eps1 = torch.from_numpy(np.random.default_rng(2).standard_normal((3, B1, cfg.latent))
+                            .astype(np.float32)).to(dev)
+    eng = Engine(c1, dev.index)
+    try:
+        eng.init_params(0)
+        P = {k: v.cpu().numpy().copy() for k, v in eng.params().items()}
+        eng.forward(x1, eps1)
+        eng.metric(a1)
+        eng.backward()
+        torch.cuda.synchronize(dev)
+        lg = eng.losses.cpu().numpy().astype(np.float64)
+        dg = eng.dist.cpu().numpy().astype(np.float64)
+        g1g = {k: v.cpu().numpy().astype(np.float64) for k, v in eng.tensors(_lib.KIND_GRAD1).items()}
+        g2g = {k: v.cpu().numpy().astype(np.float64) for k, v in eng.tensors(_lib.KIND_GRAD2).items()}
+    finally:
+        eng.close()
+    X1, A1, E1 = x1.cpu().numpy(), a1.cpu().numpy(), eps1.cpu().numpy()
+
+    def rel(a, b, mag=None):
+        s = max(np.abs(b).max(), 1e-2 * np.abs(mag).max() if mag is not None else 0.0, 1e-30)
+        return float(np.abs(np.asarray(a, np.float64) - b).max() / s)
+    c = O.forward(P, X1, E1, oc, dtype=np.float32)
+    O.metric(c, A1, oc, B1)
+    lo = O.loss_sums(c, B1)
+    g1o, g2o = O.backward(c, oc, B1)
+    m1, m2 = O.backward(c, oc, B1, magnitude=True)
+    parity = {
+        "losses": float(np.max(np.abs(lg - lo) / np.maximum(np.abs(lo), 1e-3))),
+        "distance": rel(dg, c["dist"]),
+        "grads": max(max(rel(g1g[k], g1o[k], m1[k]) for k in g1o),
+                     max(rel(g2g[k], g2o[k], m2[k]) for k in g2o)),
+    }
+    bar = 1e-4 if cfg.precision in ("f32", "f32x") else 5e-2
+
+    def timed(X, A, E, budget, min_steps=2):
+        st = O.adam_init(oc, P)
+        Pt = dict(P)
+        O.train_step(Pt, st, X, A, E, oc, dtype=np.float32)  # warm-up
+        t0 = time.perf_counter()
+        n = 0
+        while n < min_steps or time.perf_counter() - t0 < budget:
+            _, _, Pt, st, _ = O.train_step(Pt, st, X, A, E, oc, dtype=np.float32)
+            n += 1
+        dt = time.perf_counter() - t0
+        return n * X.shape[0] / dt, n, dt
+    blas = [i for i in threadpool_info() if i.get("user_api") == "blas"]
+    cores = max([i.get("num_threads", 1) for i in blas] or [1])
+    v_c1, n_c1, t_c1 = timed(X1, A1, E1, seconds)
+    with threadpool_limits(1):
+        v_c1_1, n_c1_1, t_c1_1 = timed(X1, A1, E1, seconds)
+    # the GPU-batch workload (the bench's own step shape), all threads, >= 2 steps
+    Bg = cfg.batch
+    xg, ag = synthetic_batch(Bg, cfg.image_size, seed=4243, device=dev)
+    Eg = np.random.default_rng(3).standard_normal((3, Bg, cfg.latent)).astype(np.float32)
+    v_g, n_g, t_g = timed(xg.cpu().numpy(), ag.cpu().numpy(), Eg, seconds)
+    del xg, ag
+    return {"value": round(v_g, 2), "unit": "shape-pairs/s", "cores": int(cores), "kind": "port",
+            "sample": f"oracle/mvae_oracle.py train_step (numpy float32 + {blas[0].get('internal_api', 'BLAS') if blas else 'BLAS'}), "
+                      f"{n_g} steps x {Bg} pairs of this run's step shape ({cfg.image_size}x{cfg.image_size}, "
+                      f"enc {list(cfg.enc)}, L={cfg.latent}) in {t_g:.1f} s",
+            "c1_all_threads": round(v_c1, 2), "c1_one_thread": round(v_c1_1, 2),
+            "c1_sample": f"{n_c1} / {n_c1_1} steps x {B1} pairs ({t_c1:.1f} / {t_c1_1:.1f} s)",
+            "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(),
+            "torch_threads": torch.get_num_threads(),
+            "parity_c1": {"gpu_precision": cfg.precision, "bar": bar, **{k: float(f"{v:.3g}") for k, v in parity.items()},
+                          "ok": all(v <= bar for v in parity.values()),
+                          "what": "max-norm relative GPU vs CPU, same seeded B=64 batch, eps and params: "
+                                  "5 losses, distance[B], every g1/g2 gradient (cancellation-aware)"}}
 
 
+# ------------------------------------------------------------------------ dry run
+class DryRunEngine:
+    """Launcher rehearsal only (``--dry-run``): the DataParallelStep interface on CPU tensors,
+    computing deterministic functions of the local rows (column sums / global batch) so that
+    the all-reduced result of N ranks equals one rank's on the concatenated batch. Not the
+    model, not a measurement."""
+    N_BACKWARD_PARTS = 3
+
+    def __init__(self, cfg):
+        import torch
+        self.cfg = cfg
+        L = cfg.latent
+        self.colsq = torch.zeros(2 * L, dtype=torch.float64)
+        self.coldot = torch.zeros(L, dtype=torch.float64)
+        self.grads = torch.zeros(96, dtype=torch.float64)
+        self.losses = torch.zeros(5, dtype=torch.float64)
+        self.dist = None
+
+    def forward(self, x, eps=None):
+        self.x = x.double()
+        L = self.cfg.latent
+        self.colsq.copy_((self.x[:, :2 * L] ** 2).sum(0))
+
+    def metric(self, areas):
+        inv = 1.0 / self.cfg.gbatch
+        self.losses.copy_(self.x.sum() * inv * self.losses.new_tensor([1.0, 0.5, 0.25, 0.125, 2.0]))
+        self.losses[1] += areas.double().sum() * inv
+        self.dist = self.x[:, :4].sum(1)
+        self.coldot.copy_(self.x[:, :self.cfg.latent].sum(0) * inv)
+
+    def backward_part(self, part):
+        n = self.grads.numel() // 3
+        cols = self.x[:, part * n:(part + 1) * n] * torch_arange(n, part)
+        self.grads[part * n:(part + 1) * n] = cols.sum(0) / self.cfg.gbatch
+
+    def backward(self):
+        for p in range(3):
+            self.backward_part(p)
+
+    def grad_ranges(self, part):
+        n = self.grads.numel() // 3
+        return [self.grads[part * n:(part + 1) * n]]
+
+    def adam(self):
+        pass
+
+    def predict(self, x):
+        return x.double()[:, :4].sum(1) + 1.0
+
+    def close(self):
+        pass
+
+
+def torch_arange(n, part):
+    import torch
+    return torch.arange(1 + part * n, 1 + (part + 1) * n, dtype=torch.float64)
+
+
+def dry_run_batch(cfg, world, rank, j):
+    """The global batch of draw j (seeded, identical on every rank); this rank's rows."""
+    import torch
+    g = torch.Generator().manual_seed(17 + j)
+    B = cfg.batch
+    X = (torch.rand(B * world, 3 * cfg.D, generator=g) < 0.1).float()
+    A = torch.randint(296, 6427, (B * world,), generator=g).float()
+    return X[rank * B:(rank + 1) * B].contiguous(), A[rank * B:(rank + 1) * B].contiguous()
+
+
+# ------------------------------------------------------------------------ main
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", default="C2", help="BASELINE config id (C2 fp32 B=4096 default)")
-    ap.add_argument("--batch", type=int, default=0, help="override per-GPU batch")
-    ap.add_argument("--precision", default="", help="override GEMM arithmetic: f32 | f32x | bf16")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-timing", action="store_true", help="disable per-region HIP events")
-    ap.add_argument("--region-steps", type=int, default=10,
-                    help="extra steps with every region timed (per-kernel table, dominant GEMM)")
-    ap.add_argument("--traffic-json", default=os.path.join(HERE, "profiles", "pmc_traffic.json"))
-    args = ap.parse_args()
-
+    argv = sys.argv[1:]
+    args = parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args, argv))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
 
-    from magic_amd.engine import Engine
-    from magic_amd.overlap_input import synthetic_batch
+    import torch
+    import torch.distributed as dist
+
+    from magic_amd import _lib
+    from magic_amd.config import baseline_config
     from magic_amd.parallel import DataParallelStep
+
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    if world > 1:
+        if args.dry_run:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
 
     cfg = baseline_config(args.config)
     if args.batch:
         cfg = cfg.replace(batch=args.batch)
     if args.precision:
         cfg = cfg.replace(precision=args.precision)
-    cfg = cfg.replace(global_batch=cfg.batch * world, seed=1000 + rank)
-    eng = Engine(cfg, local)
-    eng.init_params(0)  # identical replicas on every rank
-    stepper = DataParallelStep(eng, reduce_losses=True)
+    # one seed on every rank: each rank's internal sampler draws its own rows of the global
+    # batch's eps stream (Engine.set_shard via DataParallelStep)
+    cfg = cfg.replace(global_batch=cfg.batch * world)
 
-    # synthetic inputs resident in HBM: a pool of 2 batches cycled through the steps
-    pool = [synthetic_batch(cfg.batch, cfg.image_size, seed=17 + 101 * rank + j, device=dev)
-            for j in range(2)]
-    torch.cuda.synchronize()
+    if args.dry_run:
+        eng = DryRunEngine(cfg)
+        pool = [dry_run_batch(cfg, world, rank, j) for j in range(2)]
+    else:
+        from magic_amd.engine import Engine
+        from magic_amd.overlap_input import synthetic_batch
+        eng = Engine(cfg, local)
+        eng.init_params(0)  # identical replicas on every rank
+        pool = [synthetic_batch(cfg.batch, cfg.image_size, seed=17 + 101 * rank + j, device=dev)
+                for j in range(2)]
+        torch.cuda.synchronize()
+    stepper = DataParallelStep(eng, reduce_losses=True)
+    timing = not (args.no_timing or args.dry_run or args.pmc_child)
+
+    def sync():
+        if not args.dry_run:
+            torch.cuda.synchronize()
+
+    if args.pmc_child:  # profiler child: markers around the named regions, a few steps
+        names = eng.timing_names()
+        for rid in args.pmc_child.split(","):
+            eng.timing_marker(names[int(rid)], True)
+        for i in range(args.warmup + args.steps):
+            stepper.step(*pool[i % 2])
+        sync()
+        eng.close()
+        return
 
     for i in range(args.warmup):
-        x, a = pool[i % 2]
-        stepper.step(x, a)
-    torch.cuda.synchronize()
-    regions = {}
-    dom = None
-    if not args.no_timing:
+        stepper.step(*pool[i % 2])
+    sync()
+    regions, dom = {}, None
+    if timing:
         # region pass (outside the timed loop): HIP events around every region, for the
         # per-kernel table and to pick the dominant GEMM
         eng.timing_reset()
         eng.timing_enable(True)
         for i in range(args.region_steps):
-            x, a = pool[i % 2]
-            stepper.step(x, a)
-        torch.cuda.synchronize()
+            stepper.step(*pool[i % 2])
+        sync()
         eng.timing_enable(False)
         regions = eng.timing_read()
         gemms = {k: v for k, v in regions.items() if region_flops(cfg, k) > 0}
@@ -165,18 +503,19 @@ def main():
         eng.timing_enable(True)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        x, a = pool[i % 2]
-        stepper.step(x, a)
+        stepper.step(*pool[i % 2])
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     elapsed = time.perf_counter() - t0
-    eng.timing_enable(False)
-    dom_timed = eng.timing_read().get(dom) if dom else None
-    eng.timing_select(None)
+    dom_timed = None
+    if timing:
+        eng.timing_enable(False)
+        dom_timed = eng.timing_read().get(dom)
+        eng.timing_select(None)
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -186,7 +525,10 @@ def main():
         raise RuntimeError(f"non-finite losses after the timed steps: {losses}")
 
     # overlap-MSE on a held-out seeded batch (11a/main.py:94-111; 1/pred for reciprocal)
-    xe, ae = synthetic_batch(cfg.batch, cfg.image_size, seed=999, device=dev)
+    if args.dry_run:
+        xe, ae = dry_run_batch(cfg, world, rank, 99)
+    else:
+        xe, ae = synthetic_batch(cfg.batch, cfg.image_size, seed=999, device=dev)
     pred = eng.predict(xe).double()
     if cfg.reciprocal:
         pred = 1.0 / pred
@@ -195,40 +537,62 @@ def main():
     if rank == 0:
         pairs = cfg.batch * world * args.steps
         value = pairs / elapsed
-        roofline = None
+        roofline, loss_roofline = None, None
         if regions and dom_timed:
             gemms = {k: v for k, v in regions.items() if region_flops(cfg, k) > 0}
             ms_avg = dom_timed[0] / dom_timed[1]  # HIP events over the timed loop
             flops = region_flops(cfg, dom)
             achieved = flops / (ms_avg * 1e-3) / 1e12
-            peak = BF16_MFMA_PEAK_TFLOPS if cfg.precision == "bf16" else F32_MFMA_PEAK_TFLOPS
-            extra = {}
-            if cfg.precision == "f32x":
-                # the exact 3-term split runs the plane pairs (i, j), i + j < 3, as bf16 MFMA
-                # work: 6 pairs, or 3 when the A operand (the pixels) is exact in bf16. Its
-                # algorithm's FLOPs are pairs x 2MNK at the bf16 peak; the fp32-equivalent
-                # rate (2MNK / time) is reported beside it.
-                dyn = int(eng.buffer(_lib.BUF_DYN).view(torch.int32).item())
-                pairs = 3 if dom in ("enc_fwd_0", "enc_bwd_w_0") and dyn == 0 else 6
-                extra = {"fp32_equivalent_tflops": round(achieved, 2), "bf16_plane_pairs": pairs}
-                achieved *= pairs
-                flops *= pairs
-                peak = BF16_MFMA_PEAK_TFLOPS
-            traffic = None
-            try:
-                with open(args.traffic_json) as f:
-                    tj = json.load(f)
-                if (tj.get("config") == args.config and tj.get("precision") == cfg.precision
-                        and dom in tj.get("regions", {})):
-                    traffic = tj["regions"][dom]["hbm_bytes_per_launch"]
-            except (OSError, ValueError):
-                pass
+            peak = F32_MFMA_PEAK_TFLOPS if cfg.precision == "f32" else BF16_MFMA_PEAK_TFLOPS
             roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
-                        "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": traffic,
-                        "kernel": dom, "flops_per_launch": flops, "avg_ms": round(ms_avg, 4), **extra}
+                        "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                        "kernel": dom, "flops_per_launch": flops, "avg_ms": round(ms_avg, 4),
+                        "work": "algorithmic 2*M*N*K of the region's fp32 GEMM, counted once"}
+            if cfg.precision == "f32x":
+                dyn = int(eng.buffer(_lib.BUF_DYN).view(torch.int32).item())
+                pp = plane_pairs(cfg, dom, dyn == 0)
+                roofline.update({
+                    "arith": "f32x: fp32-accurate exact 3-term bf16 split on the bf16 MFMA pipe",
+                    "bf16_plane_pairs": pp,
+                    "mfma_pipe_tflops": round(achieved * pp, 2),
+                    "mfma_pipe_frac": round(achieved * pp / BF16_MFMA_PEAK_TFLOPS, 4),
+                    "frac_of_fp32_mfma_peak": round(achieved / F32_MFMA_PEAK_TFLOPS, 4)})
             rs = args.region_steps
             total_gemm_ms = sum(v[0] for v in gemms.values()) / rs
             gemm_flops = sum(region_flops(cfg, k) * v[1] for k, v in gemms.items()) / rs
+            roofline["all_gemms"] = {"ms_per_step": round(total_gemm_ms, 4),
+                                     "tflops": round(gemm_flops / total_gemm_ms / 1e9, 2)}
+            # HBM-bound kernels and the fused BCE head (north_star: achieved GB/s vs peak)
+            loss_roofline = {}
+            n_all = eng.buffer(_lib.BUF_PARAMS).numel()
+            n_enc = eng.buffer(_lib.BUF_GRADS).numel() - n_all
+            np_ = {"f32": 0, "bf16": 1, "f32x": 3}[cfg.precision]
+            for k in ("deinterleave", "eps_rng", "latent_fwd", "colsq", "metric_loss", "coldot",
+                      "latent_bwd", "adam"):
+                if k not in regions:
+                    continue
+                ms_k = regions[k][0] / regions[k][1]
+                by = adam_bytes(n_all, n_enc, np_) if k == "adam" else region_bytes(cfg, k)
+                loss_roofline[k] = {"bytes": by, "avg_ms": round(ms_k, 4),
+                                    "gbs": round(by / (ms_k * 1e-3) / 1e9, 1),
+                                    "frac": round(by / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+            lat = [k for k in ("latent_fwd", "colsq", "metric_loss", "coldot", "latent_bwd") if k in regions]
+            ms_lat = sum(regions[k][0] / regions[k][1] for k in lat)
+            by_lat = 80.0 * cfg.latent * cfg.batch
+            loss_roofline["latent_head_total"] = {
+                "kernels": lat, "avg_ms": round(ms_lat, 4), "bytes_survey": by_lat,
+                "gbs_survey": round(by_lat / (ms_lat * 1e-3) / 1e9, 1),
+                "frac_survey": round(by_lat / (ms_lat * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "note": "SURVEY.md §8d: ~80*L B/pair for the fused latent head fwd+bwd"}
+            if "dec_fwd_out_bce" in regions:
+                ms_b = regions["dec_fwd_out_bce"][0] / regions["dec_fwd_out_bce"][1]
+                by_b = 12.0 * cfg.D * cfg.batch
+                loss_roofline["bce_head"] = {
+                    "bytes": by_b, "avg_ms": round(ms_b, 4),
+                    "gbs": round(by_b / (ms_b * 1e-3) / 1e9, 1),
+                    "frac": round(by_b / (ms_b * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                    "note": "BASELINE.md §4: 12*D B/pair (logits, targets, dlogits); fused into the "
+                            "decoder-output GEMM epilogue, whose time is MFMA-bound"}
             print(f"[bench] region pass ({rs} steps): GEMM time/step {total_gemm_ms:.3f} ms, "
                   f"{gemm_flops / total_gemm_ms / 1e9:.1f} TFLOP/s over all GEMMs; timed step "
                   f"{elapsed / args.steps * 1e3:.3f} ms; {dom} {ms_avg:.4f} ms in the timed loop",
@@ -236,10 +600,24 @@ def main():
             for k, (ms, n) in sorted(regions.items(), key=lambda kv: -kv[1][0]):
                 fl = region_flops(cfg, k)
                 extra = f"  {fl / (ms / n * 1e-3) / 1e12:7.1f} TF/s" if fl else ""
+                if k in loss_roofline:
+                    extra = f"  {loss_roofline[k]['gbs']:7.1f} GB/s"
                 print(f"[bench] {k:18s} {ms / n:9.4f} ms x{n}{extra}", file=sys.stderr)
         cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(cfg, args.cpu_seconds)
+        if world == 1 and not args.no_cpu_baseline and not args.dry_run:
+            cpu = cpu_baseline(cfg, dev, args.cpu_seconds)
+        if roofline and world == 1 and args.pmc == "auto" and not args.dry_run:
+            names = eng.timing_names()
+            want = [dom] + [k for k in PMC_REGIONS_BW if k in regions]
+            tr, how = pmc_traffic(args, want, names)
+            roofline["traffic_method"] = how
+            if tr:
+                if dom in tr:
+                    roofline["traffic"] = tr[dom]["hbm_bytes"]
+                    roofline["traffic_detail"] = tr[dom]
+                for k in PMC_REGIONS_BW:
+                    if k in tr and k in loss_roofline:
+                        loss_roofline[k]["traffic"] = tr[k]["hbm_bytes"]
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -253,21 +631,30 @@ def main():
             "vs_baseline": None,
             "dtype": {"f32": "f32", "f32x": "f32 (exact 3-term bf16 split MFMA, fp32 accumulate)",
                       "bf16": "bf16 GEMM operands, fp32 accumulate"}[cfg.precision],
-            "data": "synthetic 100x100 binary shape pairs (random ellipses/rectangles, nearest-"
-                    "neighbour rotated lock), areas resampled from the reference's OVERLAP_AREAS; "
-                    "random xavier init",
+            "data": ("dry run: CPU stand-in engine, launcher rehearsal only (no GPU, not a measurement)"
+                     if args.dry_run else
+                     "synthetic 100x100 binary shape pairs (random ellipses/rectangles, nearest-"
+                     "neighbour rotated lock), areas resampled from the reference's OVERLAP_AREAS; "
+                     "random xavier init"),
             "config": {"workload": f"BASELINE {args.config}: preset "
-                                   f"{'8c' if cfg.latent == 20 else '8d/8e'} enc {list(cfg.enc)} "
-                                   f"L={cfg.latent} {cfg.act} {cfg.metric}",
+                                   f"{ {20: '8c', 200: '8d', 2000: '8e'}.get(cfg.latent, '?') } enc "
+                                   f"{list(cfg.enc)} L={cfg.latent} {cfg.act} "
+                                   f"{'reciprocal ' if cfg.reciprocal else ''}{cfg.metric}",
                        "global_batch": cfg.batch * world, "per_gpu_batch": cfg.batch,
-                       "image": f"{cfg.image_size}x{cfg.image_size}", "parallelism": f"dp{world}"},
+                       "image": f"{cfg.image_size}x{cfg.image_size}", "parallelism": f"dp{world}",
+                       "collective": ("gloo (dry run)" if args.dry_run else "RCCL all-reduce")
+                       if world > 1 else None},
             "per_gpu_value": round(value / world, 2),
             "overlap_mse": round(mse, 2),
             "losses": {"cost": losses[0], "training_loss": losses[1], "r_l": losses[2],
                        "l_l": losses[3], "d_l": losses[4]},
             "roofline": roofline,
+            "loss_roofline": loss_roofline,
             "cpu_baseline": cpu,
         }
+        if args.dry_run:
+            w = torch.arange(1, eng.grads.numel() + 1, dtype=torch.float64)
+            line["grad_checksum"] = float((eng.grads * w).sum())
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:

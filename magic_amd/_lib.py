@@ -13,6 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MVAE_LIB", os.path.join(HERE, "libmvae.so"))
 
 MVAE_MAX_ENC = 8
+MARKER_GRID = 4096   # mvae_region_marker workgroups = MARKER_GRID + region (mvae_internal.h)
 ABI_VERSION = 2
 
 ACT = {"tanh": 0, "elu": 1}
