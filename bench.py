@@ -67,6 +67,8 @@ def parse_args(argv=None):
     ap.add_argument("--pmc", default="auto", choices=["auto", "off"],
                     help="rocprofv3 FETCH_SIZE/WRITE_SIZE child passes for roofline.traffic")
     ap.add_argument("--pmc-child", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--opt", action="append", default=[],
+                    help="libmvae schedule switch NAME=VALUE (mvae_set_option), repeatable")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launcher / data-parallel / timing / JSON path "
                          "(gloo, a stand-in engine; no GPU, no kernels, not a measurement)")
@@ -216,6 +218,8 @@ def pmc_traffic(args, names, regions_all):
         child += ["--batch", str(args.batch)]
     if args.precision:
         child += ["--precision", args.precision]
+    for o in args.opt:
+        child += ["--opt", o]
     res = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = os.path.join(root, counter.lower())
@@ -460,6 +464,9 @@ def main():
         from magic_amd.engine import Engine
         from magic_amd.overlap_input import synthetic_batch
         eng = Engine(cfg, local)
+        for o in args.opt:
+            k, v = o.split("=")
+            eng.set_option(k, int(v))
         eng.init_params(0)  # identical replicas on every rank
         pool = [synthetic_batch(cfg.batch, cfg.image_size, seed=17 + 101 * rank + j, device=dev)
                 for j in range(2)]

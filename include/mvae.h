@@ -141,6 +141,10 @@ int mvae_backward(mvae_ctx* ctx, void* stream);
  * all-reduces them while the later parts run (returns MVAE_EINVAL past the last range). */
 int mvae_backward_part(mvae_ctx* ctx, int part, void* stream);
 int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* count);
+/* Schedule switches (A/B measurement): "side_stream" (default 1) runs the weight gradients
+ * on a context-owned side stream beside the dgrad chain, joined before the gradients they
+ * write are reported final (mvae_backward / the end of each mvae_backward_part). */
+int mvae_set_option(mvae_ctx* ctx, const char* name, int value);
 /* Both TF ApplyAdam updates from MVAE_BUF_GRADS (theta -= d1(g1) + d2(g2)).           */
 int mvae_adam(mvae_ctx* ctx, void* stream);
 /* Single-GPU partial_fit: all four phases. losses_out: device float[5] or NULL;

@@ -70,6 +70,7 @@ _SIGS = {
     "mvae_backward": ([C.c_void_p, C.c_void_p], C.c_int),
     "mvae_backward_part": ([C.c_void_p, C.c_int, C.c_void_p], C.c_int),
     "mvae_grad_range": ([C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)], C.c_int),
+    "mvae_set_option": ([C.c_void_p, C.c_char_p, C.c_int], C.c_int),
     "mvae_adam": ([C.c_void_p, C.c_void_p], C.c_int),
     "mvae_train_step": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                          C.c_void_p], C.c_int),

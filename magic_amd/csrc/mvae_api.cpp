@@ -61,8 +61,18 @@ struct mvae_ctx {
   std::vector<float*> dzl;  // dZ of every encoder layer [4B][lddz] (all live until its wgrad)
   int enc_part1 = 0;        // bwd_enc[0, enc_part1): dgrad chain + layer-0 wgrad
   float* zgen = nullptr;
-  float* ws = nullptr;
+  float* ws = nullptr;       // split-K slabs of GEMMs on the caller's stream
+  float* ws_side = nullptr;  // ... and of GEMMs on the side stream (concurrent)
   size_t ws_elems = 0;
+  int* cnt = nullptr;        // split-K tile tickets of the caller's stream (zero between GEMMs)
+  int* cnt_side = nullptr;   // ... and of the side stream
+  bool fixup = true;         // option "splitk_fixup": in-launch split-K combine
+  // side stream: the weight gradients run beside the dgrad chain (backward)
+  hipStream_t side = nullptr;
+  std::vector<hipEvent_t> sync_ev;  // fork/join events (timing disabled), reused round robin
+  size_t sync_next = 0;
+  bool use_side = true;      // option "side_stream"
+  bool side_pending = false; // side stream holds work the caller's stream has not joined
   std::vector<void*> allocs;
   // bf16 plane images (bf16 / f32x modes): fp32 buffer -> planes of the same layout
   struct PlaneBuf { float* base; size_t n; Planes pl; };
@@ -323,6 +333,8 @@ int mvae_destroy(mvae_ctx* ctx) {
   hipDeviceSynchronize();
   for (auto& pd : ctx->pending) { hipEventDestroy(pd.a); hipEventDestroy(pd.b); }
   for (auto e : ctx->event_pool) hipEventDestroy(e);
+  for (auto e : ctx->sync_ev) hipEventDestroy(e);
+  if (ctx->side) hipStreamDestroy(ctx->side);
   for (void* p : ctx->allocs) hipFree(p);
   hipSetDevice(dev);
   delete ctx;
@@ -533,14 +545,38 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
         return MVAE_EINVAL;
       }
   size_t ws = 0;
-  for (auto& d : c->fwd_enc) ws = std::max(ws, gemm_workspace_elems(d));
-  for (auto& d : c->bwd_dec) ws = std::max(ws, gemm_workspace_elems(d));
-  for (auto& d : c->bwd_enc) ws = std::max(ws, gemm_workspace_elems(d));
-  ws = std::max(ws, gemm_workspace_elems(c->f_d1));
-  ws = std::max(ws, gemm_workspace_elems(c->f_d2));
+  auto wsz = [&](const GemmDesc& d) {
+    GemmDesc a = d, b = d;
+    a.fixup = 1; b.fixup = 0;  // both combine modes (switchable at run time)
+    ws = std::max(ws, std::max(gemm_workspace_elems(a), gemm_workspace_elems(b)));
+  };
+  for (auto& d : c->fwd_enc) wsz(d);
+  for (auto& d : c->bwd_dec) wsz(d);
+  for (auto& d : c->bwd_enc) wsz(d);
+  wsz(c->f_d1);
+  wsz(c->f_d2);
+  wsz(c->f_out);
   c->ws_elems = ws;
   ALLOC(c->ws, ws);
+  ALLOC(c->ws_side, ws);
+  ALLOC(*reinterpret_cast<float**>(&c->cnt), GEMM_MAX_TILES);       // zeroed by dalloc
+  ALLOC(*reinterpret_cast<float**>(&c->cnt_side), GEMM_MAX_TILES);
 #undef ALLOC
+  {
+    int lo = 0, hi = 0;
+    hipError_t se = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (se == hipSuccess) se = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, lo);
+    for (int i = 0; se == hipSuccess && i < 16; ++i) {
+      hipEvent_t ev = nullptr;
+      se = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+      if (se == hipSuccess) c->sync_ev.push_back(ev);
+    }
+    if (se != hipSuccess) {
+      g_create_err = std::string("side stream: ") + hipGetErrorString(se);
+      mvae_destroy(c);
+      return (int)se;
+    }
+  }
   *out = c;
   return MVAE_OK;
 }
@@ -680,7 +716,18 @@ int mvae_sync_params(mvae_ctx* ctx, void* stream) {
 // ------------------------------------------------------------------ phases
 static int run(mvae_ctx* ctx, const GemmDesc& d, hipStream_t st, int r = -1) {
   TimeScope ts(ctx, r < 0 ? region(ctx, "other_gemm") : r, st);
-  MV_CHECK(gemm_run(d, ctx->ws, ctx->ws_elems, st));
+  const bool sd = st == ctx->side && ctx->side;
+  GemmDesc g = d;
+  g.fixup = ctx->fixup;
+  MV_CHECK(gemm_run(g, sd ? ctx->ws_side : ctx->ws, ctx->ws_elems, st, sd ? ctx->cnt_side : ctx->cnt));
+  return MVAE_OK;
+}
+
+// `to` waits for the work enqueued on `from` so far
+static int stream_wait(mvae_ctx* ctx, hipStream_t from, hipStream_t to) {
+  hipEvent_t ev = ctx->sync_ev[ctx->sync_next++ % ctx->sync_ev.size()];
+  MV_CHECK(hipEventRecord(ev, from));
+  MV_CHECK(hipStreamWaitEvent(to, ev, 0));
   return MVAE_OK;
 }
 #define TIMED(name) TimeScope ts_##__LINE__(ctx, region(ctx, name), st)
@@ -762,18 +809,37 @@ extern "C" int mvae_metric(mvae_ctx* ctx, const float* areas, void* stream) {
 }
 
 // Backward in three parts (phase 2 -> 4 -> 5 -> 3); after part k the ranges
-// mvae_grad_range(ctx, k, i, ...) hold final (rank-local) gradients.
-extern "C" int mvae_backward_part(mvae_ctx* ctx, int part, void* stream) {
-  if (!ctx) return MVAE_EINVAL;
-  const int need = part == 0 ? 2 : (part == 1 ? 4 : 5);
-  if (part < 0 || part > 2) return fail(ctx, MVAE_EINVAL, "backward part must be 0, 1 or 2");
-  if (ctx->phase != need) return fail(ctx, MVAE_ESTATE, "mvae_backward_part out of order");
-  hipStream_t st = (hipStream_t)stream;
+// mvae_grad_range(ctx, k, i, ...) hold final (rank-local) gradients on the caller's stream.
+// The dgrad chain (decoder output -> ... -> encoder layer 1) runs on the caller's stream; each
+// weight gradient runs on the side stream as soon as its dZ exists, beside the chain (the
+// chain's GEMMs leave CUs idle: few tiles, split-K reductions). Part 0 joins the decoder's
+// weight gradients, part 2 the encoder's (part 1 ends with the layer-0 weight gradient on the
+// caller's stream). join_dec = false (the single-call mvae_backward) leaves the decoder's
+// weight gradients running beside the encoder chain too.
+static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec) {
   auto c = ctx;
   int rc;
+  const bool two = c->use_side && c->side;
+  hipStream_t sd = two ? c->side : st;
+  auto fork = [&]() -> int { return two ? stream_wait(c, st, sd) : MVAE_OK; };
+  auto join = [&]() -> int {
+    if (!two || !c->side_pending) return MVAE_OK;
+    c->side_pending = false;
+    return stream_wait(c, sd, st);
+  };
   if (part == 0) {
-    for (size_t i = 0; i < c->bwd_dec.size(); ++i)
-      if ((rc = run(c, c->bwd_dec[i], st, c->bwd_dec_r[i]))) return rc;
+    // bwd_dec: W_out, D_out, W_d2, D_d2, W_d1, D_z
+    if ((rc = fork())) return rc;
+    c->side_pending = two;
+    if ((rc = run(c, c->bwd_dec[0], sd, c->bwd_dec_r[0]))) return rc;
+    if ((rc = run(c, c->bwd_dec[1], st, c->bwd_dec_r[1]))) return rc;
+    if ((rc = fork())) return rc;
+    if ((rc = run(c, c->bwd_dec[2], sd, c->bwd_dec_r[2]))) return rc;
+    if ((rc = run(c, c->bwd_dec[3], st, c->bwd_dec_r[3]))) return rc;
+    if ((rc = fork())) return rc;
+    if ((rc = run(c, c->bwd_dec[4], sd, c->bwd_dec_r[4]))) return rc;
+    if ((rc = run(c, c->bwd_dec[5], st, c->bwd_dec_r[5]))) return rc;
+    if (join_dec && (rc = join())) return rc;
     ctx->phase = 4;
   } else if (part == 1) {
     {
@@ -782,15 +848,37 @@ extern "C" int mvae_backward_part(mvae_ctx* ctx, int part, void* stream) {
                                  c->B, c->L, c->cfg.metric, c->cfg.deform_weight, c->inv_bg, c->dhead,
                                  c->ld_dh, planes_of(c, c->dhead), st));
     }
-    for (int i = 0; i < c->enc_part1; ++i)
-      if ((rc = run(c, c->bwd_enc[i], st, c->bwd_enc_r[i]))) return rc;
+    // bwd_enc: [dgrad(n) .. dgrad(1), wgrad(0) | wgrad(n), wgrad(n-1) .. wgrad(1)]; dgrad(i)
+    // produces dZ_{i-1}, wgrad(i) needs dZ_i (dgrad(n) = the head's: dZ of layer n-1)
+    const int n = c->nenc;
+    auto wg = [&](int i) -> const GemmDesc& { return c->bwd_enc[c->enc_part1 + (n - i)]; };
+    auto wr = [&](int i) { return c->bwd_enc_r[c->enc_part1 + (n - i)]; };
+    if ((rc = fork())) return rc;
+    c->side_pending = two;
+    if ((rc = run(c, wg(n), sd, wr(n)))) return rc;  // head weight gradient (dhead)
+    for (int j = 0; j < n; ++j) {
+      const int i = n - j;  // dgrad(i) -> dZ_{i-1}
+      if ((rc = run(c, c->bwd_enc[j], st, c->bwd_enc_r[j]))) return rc;
+      if (i - 1 >= 1) {
+        if ((rc = fork())) return rc;
+        if ((rc = run(c, wg(i - 1), sd, wr(i - 1)))) return rc;
+      }
+    }
+    if ((rc = run(c, c->bwd_enc[n], st, c->bwd_enc_r[n]))) return rc;  // wgrad(0)
     ctx->phase = 5;
   } else {
-    for (size_t i = c->enc_part1; i < c->bwd_enc.size(); ++i)
-      if ((rc = run(c, c->bwd_enc[i], st, c->bwd_enc_r[i]))) return rc;
+    if ((rc = join())) return rc;
     ctx->phase = 3;
   }
   return MVAE_OK;
+}
+
+extern "C" int mvae_backward_part(mvae_ctx* ctx, int part, void* stream) {
+  if (!ctx) return MVAE_EINVAL;
+  const int need = part == 0 ? 2 : (part == 1 ? 4 : 5);
+  if (part < 0 || part > 2) return fail(ctx, MVAE_EINVAL, "backward part must be 0, 1 or 2");
+  if (ctx->phase != need) return fail(ctx, MVAE_ESTATE, "mvae_backward_part out of order");
+  return backward_part(ctx, part, (hipStream_t)stream, true);
 }
 
 extern "C" int mvae_backward(mvae_ctx* ctx, void* stream) {
@@ -798,8 +886,16 @@ extern "C" int mvae_backward(mvae_ctx* ctx, void* stream) {
   if (ctx->phase != 2) return fail(ctx, MVAE_ESTATE, "mvae_backward before mvae_metric");
   int rc;
   for (int part = 0; part < 3; ++part)
-    if ((rc = mvae_backward_part(ctx, part, stream))) return rc;
+    if ((rc = backward_part(ctx, part, (hipStream_t)stream, false))) return rc;
   return MVAE_OK;
+}
+
+extern "C" int mvae_set_option(mvae_ctx* ctx, const char* name, int value) {
+  if (!ctx || !name) return MVAE_EINVAL;
+  const std::string k(name);
+  if (k == "side_stream") { ctx->use_side = value != 0; return MVAE_OK; }
+  if (k == "splitk_fixup") { ctx->fixup = value != 0; return MVAE_OK; }
+  return fail(ctx, MVAE_EINVAL, "unknown option " + k);
 }
 
 extern "C" int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* count) {
@@ -918,7 +1014,8 @@ extern "C" int mvae_generate(mvae_ctx* ctx, const float* zin, int n, float* y_ou
 extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int at, const float* Bm,
                                int ldb, int bt, float* Cm, int ldc, int epi, int act, const float* aux,
                                int ld_aux, void* stream) {
-  if ((epi & 15) == EPI_BCE || epi < 0 || (epi & 15) > EPI_SIGMOID || ((epi >> 4) & 15) > 2)
+  if ((epi & 15) == EPI_BCE || epi < 0 || (epi & 15) > EPI_SIGMOID || ((epi >> 4) & 15) > 2 ||
+      ((epi >> 13) & 7) > 4)
     return fail(nullptr, MVAE_EINVAL, "bad epilogue");
   hipStream_t st = (hipStream_t)stream;
   GemmDesc d = gd(M, N, K, A, lda, at != 0, Bm, ldb, bt != 0, Cm, ldc, epi & 15);
@@ -942,12 +1039,19 @@ extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int
     d.Ap = A_.p; d.pA = A_.stride; d.nA = np;
     d.Bp = B_.p; d.pB = B_.stride; d.nB = np;
   }
-  const size_t ws_n = gemm_workspace_elems(d);
+  d.fixup = ((epi >> 12) & 1) ? 0 : 1;  // bit 12: separate split-K reduction kernel
+  d.split = (epi >> 13) & 7;            // bits 13-15: forced split (0: planner)
+  const size_t ws_n = gemm_workspace_elems(d) + (d.split ? (size_t)d.batch * 8 * 65536 *
+                                                 ((M + 255) / 256) * ((N + 255) / 256) : 0);
   float* ws = nullptr;
+  int* cnt = nullptr;
   if (e == hipSuccess && ws_n) e = hipMalloc(&ws, ws_n * sizeof(float));
-  if (e == hipSuccess) e = gemm_run(d, ws, ws_n, st);
+  if (e == hipSuccess) e = hipMalloc(&cnt, GEMM_MAX_TILES * sizeof(int));
+  if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, GEMM_MAX_TILES * sizeof(int), st);
+  if (e == hipSuccess) e = gemm_run(d, ws, ws_n, st, cnt);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (ws) (void)hipFree(ws);
+  if (cnt) (void)hipFree(cnt);
   for (void* q : tmp) if (q) (void)hipFree(q);
   if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
   return MVAE_OK;
@@ -1066,14 +1170,18 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
       d.epi.cp = cpl; d.epi.pc = (long long)nc; d.epi.ncp = np;
     }
   }
+  d.fixup = ((variant >> 12) & 1) ? 0 : 1;  // bit 12: separate split-K reduction kernel
   const size_t ws_n = gemm_workspace_elems(d);
+  int* cnt = nullptr;
   if (e == hipSuccess && ws_n) e = hipMalloc(&ws, ws_n * 4);
+  if (e == hipSuccess) e = hipMalloc(&cnt, GEMM_MAX_TILES * sizeof(int));
+  if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, GEMM_MAX_TILES * sizeof(int), st);
   hipEvent_t t0 = nullptr, t1 = nullptr;
   if (e == hipSuccess) e = hipEventCreate(&t0);
   if (e == hipSuccess) e = hipEventCreate(&t1);
-  for (int i = 0; e == hipSuccess && i < 3; ++i) e = gemm_run(d, ws, ws_n, st);
+  for (int i = 0; e == hipSuccess && i < 3; ++i) e = gemm_run(d, ws, ws_n, st, cnt);
   if (e == hipSuccess) e = hipEventRecord(t0, st);
-  for (int i = 0; e == hipSuccess && i < iters; ++i) e = gemm_run(d, ws, ws_n, st);
+  for (int i = 0; e == hipSuccess && i < iters; ++i) e = gemm_run(d, ws, ws_n, st, cnt);
   if (e == hipSuccess) e = hipEventRecord(t1, st);
   if (e == hipSuccess) e = hipEventSynchronize(t1);
   float ms = 0.f;
@@ -1084,6 +1192,7 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   for (float* p : {A, Bm, Cm, ws, aux, rowpart}) if (p) (void)hipFree(p);
   if (planes) (void)hipFree(planes);
   if (cpl) (void)hipFree(cpl);
+  if (cnt) (void)hipFree(cnt);
   if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
   return MVAE_OK;
 }

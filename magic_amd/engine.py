@@ -210,6 +210,9 @@ class Engine:
                 out.append(self.grads[off:off + n.value])
         return out
 
+    def set_option(self, name: str, value: int):
+        self._check(self.lib.mvae_set_option(self.ctx, name.encode(), int(value)))
+
     def adam(self):
         self._check(self.lib.mvae_adam(self.ctx, self.stream))
 
