@@ -404,9 +404,6 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16w_kernel(PParams pp) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (p.slab != nullptr && p.split > 1 &&
-      !splitk_fixup<4, 2, WT>(p, t, acc, reinterpret_cast<int*>(smem) + DEPTH * IMG - 4))
-    return;
   // C/D-layout epilogue: one 128-B row segment per half-wave store. (An LDS-transposed form
   // with 16-B row stores measured slower on every step shape and spills with BCE.)
   epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
@@ -530,11 +527,6 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16r_kernel(PParams pp) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // split-K: the tile's last-arriving K-slice combines the slices (the ticket flag sits in the
-  // last 16 B of the LDS array, past the BCE epilogue's row-partial scratch)
-  if (p.slab != nullptr && p.split > 1 &&
-      !splitk_fixup<4, 2, WT>(p, t, acc, reinterpret_cast<int*>(smem) + 5 * IMG / 2 - 4))
-    return;
   epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
 }
 
@@ -628,8 +620,7 @@ bool gemm_bf16_wide(const GemmDesc& d) {
 }
 
 int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws) {
-  const bool bce = d.epi.mode == EPI_BCE || d.epi.mode == EPI_BCEB || d.epi.mode == EPI_SIGMOID;
-  if (bce && !d.fixup) return 1;  // the reduction kernel has no BCE / sigmoid epilogue
+  if (d.epi.mode == EPI_BCE || d.epi.mode == EPI_BCEB || d.epi.mode == EPI_SIGMOID) return 1;
   const long long tiles = (long long)((d.M + WT - 1) / WT) * ((d.N + WT - 1) / WT) * d.batch;
   const int kt = (d.K + 63) / 64;
   const int T = d.nA > d.nB ? d.nA : d.nB;
@@ -637,24 +628,17 @@ int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws) {
   for (int i = 0; i < d.nA; ++i)
     for (int j = 0; j < d.nB; ++j) np += i + j < T;
   if (d.dynA) np = (np + (d.nB < T ? d.nB : T)) / 2;  // A's residual planes often all zero
-  // one 256x256x64 k-tile per CU (one workgroup per CU); + prologue/epilogue. Split-K adds
-  // either the in-launch combine (each slice stores a 256 KB fp32 partial write-through, the
-  // last-arriving one reads the others back) or the fp32 slab round trip + a reduction launch.
+  // one 256x256x64 k-tile per CU (one workgroup per CU); + prologue/epilogue;
+  // split-K adds the fp32 slab round trip and the reduction launch
   const double t_kt = 1.9e-6;  // measured: 4096^3 at 1.06 PF/s = 1.94 us per k-tile per CU
-  const int smax = d.fixup ? 4 : 32;
   double best = 1e30;
   int best_s = 1;
-  for (int s = 1; s <= smax; ++s) {
+  for (int s = 1; s <= 32; ++s) {
     if (s > 1 && kt / s < 2) break;
-    const size_t need = d.fixup ? (size_t)tiles * s * WT * WT : (size_t)d.batch * s * d.M * d.N;
-    if (s > 1 && need > max_ws) break;
-    if (s > 1 && d.fixup && tiles > GEMM_MAX_TILES) break;
+    if (s > 1 && (size_t)d.batch * s * d.M * d.N > max_ws) break;
     const double rounds = std::ceil(tiles * s / 256.0);
     double t = rounds * (np * std::ceil((double)kt / s) + 3.0) * t_kt;
-    if (s > 1) {
-      t += d.fixup ? rounds * (1.0 + 0.6 * s) * 1e-6
-                   : (double)d.batch * s * d.M * d.N * 8.0 / 4.5e12 + 4e-6;
-    }
+    if (s > 1) t += (double)d.batch * s * d.M * d.N * 8.0 / 4.5e12 + 4e-6;
     if (t < best * 0.97) { best = t; best_s = s; }
   }
   return best_s;

@@ -21,8 +21,6 @@ struct Params {
   int batch, split, kchunk;
   int ntm, ntn;
   GemmEpi epi;
-  float* slab;              // split-K in-launch combine: per-tile slice partials (or nullptr)
-  int* cnt;                 // ... and per-tile arrival tickets (zero between launches)
 };
 
 __device__ __forceinline__ float act_f(float v, int act) {
@@ -103,82 +101,6 @@ __device__ __forceinline__ Tile tile_of_t(const Params& p, bool remap) {
 }
 __device__ __forceinline__ Tile tile_of(const Params& p, bool remap) {
   return tile_of_t<BM, BN>(p, remap);
-}
-
-// In-launch split-K combine (cdna_hip_programming.md §5 'Projection GEMM', item 2, write-through
-// form): every K-slice workgroup of a tile stores its fp32 partial accumulators with 16-B sc1
-// (write-through) buffer stores in fragment order, drains them (vmcnt(0) in every wave), and
-// lane 0 takes a relaxed agent-scope ticket. The workgroup drawing the last ticket reads every
-// slice back with sc1 loads (no stale L1/L2 copy can be hit, whatever the XCD placement), sums
-// them in SLICE order (results independent of arrival order: bitwise deterministic), resets the
-// ticket and returns true to run the epilogue; the others return false. flag: an int in the
-// kernel's LDS array that the epilogue does not use. split <= 4.
-template <int MI, int NI, int TBM>
-__device__ __forceinline__ bool splitk_fixup(const Params& p, const Tile& t, f32x16 (&acc)[MI][NI],
-                                             int* flag) {
-  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-  constexpr int Q = MI * NI * 4;  // 16-B chunks of accumulators per thread
-  const int tid = threadIdx.x, nt = blockDim.x;
-  const long long tl = ((long long)t.bi * p.ntm + t.m0 / TBM) * p.ntn + t.nt;
-  const int per = Q * 16 * nt;    // bytes of one slice
-  float* base = p.slab + (size_t)tl * p.split * (per / 4);
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base, (short)0, p.split * per,
-                                                                       0x00020000);
-  const int off0 = tid * 16;
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        const int q = (mi * NI + ni) * 4 + r4;
-        const u32x4 v = {__float_as_uint(acc[mi][ni][4 * r4]), __float_as_uint(acc[mi][ni][4 * r4 + 1]),
-                         __float_as_uint(acc[mi][ni][4 * r4 + 2]), __float_as_uint(acc[mi][ni][4 * r4 + 3])};
-        __builtin_amdgcn_raw_buffer_store_b128(v, rs, t.si * per + q * nt * 16 + off0, 0, 16);
-      }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const int old = __hip_atomic_fetch_add(p.cnt + tl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = old == p.split - 1;
-  }
-  __syncthreads();
-  const bool last = *flag != 0;
-  if (!last) return false;
-  // slices other than this one: j -> slice j + (j >= si), loaded unconditionally (a slice past
-  // the last is outside the descriptor's range: the load returns 0 without a memory access);
-  // folded in slice order with value selects (a select between a register and a LOAD, or a
-  // branch around loads, makes hipcc serialise them)
-  const int si = t.si, ns = p.split;
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      u32x4 o0[4], o1[4], o2[4];
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4) {
-        const int q = (mi * NI + ni) * 4 + r4;
-        const int qo = q * nt * 16 + off0;
-        o0[r4] = __builtin_amdgcn_raw_buffer_load_b128(rs, (0 + (0 >= si)) * per + qo, 0, 16);
-        o1[r4] = __builtin_amdgcn_raw_buffer_load_b128(rs, (1 + (1 >= si)) * per + qo, 0, 16);
-        o2[r4] = __builtin_amdgcn_raw_buffer_load_b128(rs, (2 + (2 >= si)) * per + qo, 0, 16);
-      }
-#pragma unroll
-      for (int r4 = 0; r4 < 4; ++r4)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float mine = acc[mi][ni][4 * r4 + e];
-          const float a0 = __uint_as_float(o0[r4][e]), a1 = __uint_as_float(o1[r4][e]),
-                      a2 = __uint_as_float(o2[r4][e]);
-          float tot = si == 0 ? mine : a0;                       // slice 0
-          tot += si == 1 ? mine : (si < 1 ? a0 : a1);            // slice 1 (ns >= 2)
-          if (ns > 2) tot += si == 2 ? mine : (si < 2 ? a1 : a2);  // slice 2
-          if (ns > 3) tot += si == 3 ? mine : a2;                // slice 3
-          acc[mi][ni][4 * r4 + e] = tot;
-        }
-    }
-  if (tid == 0) __hip_atomic_store(p.cnt + tl, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return true;
 }
 
 // Epilogue over this wave's MI x NI 32x32 accumulators; the wave owns rows

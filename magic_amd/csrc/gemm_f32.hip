@@ -344,17 +344,10 @@ int gemm_plan_split(const GemmDesc& d, size_t max_ws) {
 
 size_t gemm_workspace_elems(const GemmDesc& d) {
   const int s = gemm_plan_split(d, ~size_t(0));
-  if (s <= 1) return 0;
-  if (d.fixup && gemm_bf16_wide(d)) {  // one 256x256 fp32 partial per (tile, slice)
-    const long long tiles = (long long)((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
-    return (size_t)tiles * s * 256 * 256;
-  }
-  return (size_t)d.batch * s * d.M * d.N;
+  return s > 1 ? (size_t)d.batch * s * d.M * d.N : 0;
 }
 
-hipError_t gemm_run(const GemmDesc& d0, float* ws, size_t ws_elems, hipStream_t st, int* cnt) {
-  GemmDesc d = d0;
-  if (!cnt) d.fixup = 0;  // no ticket array: the separate reduction kernel combines split-K
+hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t st) {
   if (d.M <= 0 || d.N <= 0) return hipSuccess;
   Params p;
   p.M = d.M; p.N = d.N; p.K = d.K;
@@ -363,17 +356,14 @@ hipError_t gemm_run(const GemmDesc& d0, float* ws, size_t ws_elems, hipStream_t 
   p.batch = d.batch;
   p.ntm = (d.M + BM - 1) / BM; p.ntn = (d.N + BN - 1) / BN;
   p.epi = d.epi;
-  p.slab = nullptr; p.cnt = nullptr;
   if (d.prec == GEMM_F32) p.epi.xdyn = nullptr;  // fp32 kernels read the fp32 BCE target
   const int split = d.split > 0 ? d.split : gemm_plan_split(d, ws ? ws_elems : 0);
   p.split = split;
   const int kb = d.prec == GEMM_F32 ? BK : 64;  // k-tile of the kernel that runs
   const int ktiles = (d.K + kb - 1) / kb;
   p.kchunk = ((ktiles + split - 1) / split) * kb;
-  const bool fix = split > 1 && d.fixup && d.prec != GEMM_F32 && gemm_bf16_wide(d) && split <= 4;
-  if (split == 1 || fix) {
+  if (split == 1) {
     p.C = d.C; p.ldc = d.ldc; p.sC = d.sC;
-    if (fix) { p.slab = ws; p.cnt = cnt; }
     if (d.prec != GEMM_F32) {
       // BCE with a bf16-plane target: two launches, each running only for its *xdyn state
       if (d.epi.mode == EPI_BCE && d.epi.xp && d.epi.xdyn) {
@@ -393,7 +383,6 @@ hipError_t gemm_run(const GemmDesc& d0, float* ws, size_t ws_elems, hipStream_t 
       default: return hipErrorInvalidValue;
     }
   }
-  if (d.epi.mode == EPI_BCE || d.epi.mode == EPI_BCEB) return hipErrorInvalidValue;
   // split-K: raw slabs [batch][split][M][N], then ordered reduction + epilogue
   p.C = ws; p.ldc = d.N; p.sC = (long long)d.M * d.N;
   p.epi.cp = nullptr;  // planes (and the fp32 output, if any) are written by the reduction

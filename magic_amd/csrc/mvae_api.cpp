@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -64,9 +65,6 @@ struct mvae_ctx {
   float* ws = nullptr;       // split-K slabs of GEMMs on the caller's stream
   float* ws_side = nullptr;  // ... and of GEMMs on the side stream (concurrent)
   size_t ws_elems = 0;
-  int* cnt = nullptr;        // split-K tile tickets of the caller's stream (zero between GEMMs)
-  int* cnt_side = nullptr;   // ... and of the side stream
-  bool fixup = true;         // option "splitk_fixup": in-launch split-K combine
   // side stream: the weight gradients run beside the dgrad chain (backward)
   hipStream_t side = nullptr;
   std::vector<hipEvent_t> sync_ev;  // fork/join events (timing disabled), reused round robin
@@ -545,11 +543,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
         return MVAE_EINVAL;
       }
   size_t ws = 0;
-  auto wsz = [&](const GemmDesc& d) {
-    GemmDesc a = d, b = d;
-    a.fixup = 1; b.fixup = 0;  // both combine modes (switchable at run time)
-    ws = std::max(ws, std::max(gemm_workspace_elems(a), gemm_workspace_elems(b)));
-  };
+  auto wsz = [&](const GemmDesc& d) { ws = std::max(ws, gemm_workspace_elems(d)); };
   for (auto& d : c->fwd_enc) wsz(d);
   for (auto& d : c->bwd_dec) wsz(d);
   for (auto& d : c->bwd_enc) wsz(d);
@@ -557,10 +551,21 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   wsz(c->f_d2);
   wsz(c->f_out);
   c->ws_elems = ws;
+  if (const char* lg = std::getenv("MVAE_PLAN_LOG"); lg && *lg == '1') {
+    // the GEMM plans of this context (diagnostics): shape, arithmetic, kernel, split-K + combine
+    auto show = [&](const GemmDesc& d, int r) {
+      const int sp = gemm_plan_split(d, ws);
+      std::fprintf(stderr, "[mvae plan] %-16s M %6d N %6d K %6d batch %d prec %d wide %d split %d\n",
+                   r >= 0 ? c->region_names[r].c_str() : "?", d.M, d.N, d.K, d.batch, d.prec,
+                   (int)gemm_bf16_wide(d), sp);
+    };
+    for (size_t i = 0; i < c->fwd_enc.size(); ++i) show(c->fwd_enc[i], c->fwd_enc_r[i]);
+    show(c->f_d1, c->f_d1_r); show(c->f_d2, c->f_d2_r); show(c->f_out, c->f_out_r);
+    for (size_t i = 0; i < c->bwd_dec.size(); ++i) show(c->bwd_dec[i], c->bwd_dec_r[i]);
+    for (size_t i = 0; i < c->bwd_enc.size(); ++i) show(c->bwd_enc[i], c->bwd_enc_r[i]);
+  }
   ALLOC(c->ws, ws);
   ALLOC(c->ws_side, ws);
-  ALLOC(*reinterpret_cast<float**>(&c->cnt), GEMM_MAX_TILES);       // zeroed by dalloc
-  ALLOC(*reinterpret_cast<float**>(&c->cnt_side), GEMM_MAX_TILES);
 #undef ALLOC
   {
     int lo = 0, hi = 0;
@@ -717,9 +722,7 @@ int mvae_sync_params(mvae_ctx* ctx, void* stream) {
 static int run(mvae_ctx* ctx, const GemmDesc& d, hipStream_t st, int r = -1) {
   TimeScope ts(ctx, r < 0 ? region(ctx, "other_gemm") : r, st);
   const bool sd = st == ctx->side && ctx->side;
-  GemmDesc g = d;
-  g.fixup = ctx->fixup;
-  MV_CHECK(gemm_run(g, sd ? ctx->ws_side : ctx->ws, ctx->ws_elems, st, sd ? ctx->cnt_side : ctx->cnt));
+  MV_CHECK(gemm_run(d, sd ? ctx->ws_side : ctx->ws, ctx->ws_elems, st));
   return MVAE_OK;
 }
 
@@ -894,7 +897,6 @@ extern "C" int mvae_set_option(mvae_ctx* ctx, const char* name, int value) {
   if (!ctx || !name) return MVAE_EINVAL;
   const std::string k(name);
   if (k == "side_stream") { ctx->use_side = value != 0; return MVAE_OK; }
-  if (k == "splitk_fixup") { ctx->fixup = value != 0; return MVAE_OK; }
   return fail(ctx, MVAE_EINVAL, "unknown option " + k);
 }
 
@@ -1014,8 +1016,7 @@ extern "C" int mvae_generate(mvae_ctx* ctx, const float* zin, int n, float* y_ou
 extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int at, const float* Bm,
                                int ldb, int bt, float* Cm, int ldc, int epi, int act, const float* aux,
                                int ld_aux, void* stream) {
-  if ((epi & 15) == EPI_BCE || epi < 0 || (epi & 15) > EPI_SIGMOID || ((epi >> 4) & 15) > 2 ||
-      ((epi >> 13) & 7) > 4)
+  if ((epi & 15) == EPI_BCE || epi < 0 || (epi & 15) > EPI_SIGMOID || ((epi >> 4) & 15) > 2)
     return fail(nullptr, MVAE_EINVAL, "bad epilogue");
   hipStream_t st = (hipStream_t)stream;
   GemmDesc d = gd(M, N, K, A, lda, at != 0, Bm, ldb, bt != 0, Cm, ldc, epi & 15);
@@ -1039,19 +1040,12 @@ extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int
     d.Ap = A_.p; d.pA = A_.stride; d.nA = np;
     d.Bp = B_.p; d.pB = B_.stride; d.nB = np;
   }
-  d.fixup = ((epi >> 12) & 1) ? 0 : 1;  // bit 12: separate split-K reduction kernel
-  d.split = (epi >> 13) & 7;            // bits 13-15: forced split (0: planner)
-  const size_t ws_n = gemm_workspace_elems(d) + (d.split ? (size_t)d.batch * 8 * 65536 *
-                                                 ((M + 255) / 256) * ((N + 255) / 256) : 0);
+  const size_t ws_n = gemm_workspace_elems(d);
   float* ws = nullptr;
-  int* cnt = nullptr;
   if (e == hipSuccess && ws_n) e = hipMalloc(&ws, ws_n * sizeof(float));
-  if (e == hipSuccess) e = hipMalloc(&cnt, GEMM_MAX_TILES * sizeof(int));
-  if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, GEMM_MAX_TILES * sizeof(int), st);
-  if (e == hipSuccess) e = gemm_run(d, ws, ws_n, st, cnt);
+  if (e == hipSuccess) e = gemm_run(d, ws, ws_n, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
   if (ws) (void)hipFree(ws);
-  if (cnt) (void)hipFree(cnt);
   for (void* q : tmp) if (q) (void)hipFree(q);
   if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
   return MVAE_OK;
@@ -1170,18 +1164,14 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
       d.epi.cp = cpl; d.epi.pc = (long long)nc; d.epi.ncp = np;
     }
   }
-  d.fixup = ((variant >> 12) & 1) ? 0 : 1;  // bit 12: separate split-K reduction kernel
   const size_t ws_n = gemm_workspace_elems(d);
-  int* cnt = nullptr;
   if (e == hipSuccess && ws_n) e = hipMalloc(&ws, ws_n * 4);
-  if (e == hipSuccess) e = hipMalloc(&cnt, GEMM_MAX_TILES * sizeof(int));
-  if (e == hipSuccess) e = hipMemsetAsync(cnt, 0, GEMM_MAX_TILES * sizeof(int), st);
   hipEvent_t t0 = nullptr, t1 = nullptr;
   if (e == hipSuccess) e = hipEventCreate(&t0);
   if (e == hipSuccess) e = hipEventCreate(&t1);
-  for (int i = 0; e == hipSuccess && i < 3; ++i) e = gemm_run(d, ws, ws_n, st, cnt);
+  for (int i = 0; e == hipSuccess && i < 3; ++i) e = gemm_run(d, ws, ws_n, st);
   if (e == hipSuccess) e = hipEventRecord(t0, st);
-  for (int i = 0; e == hipSuccess && i < iters; ++i) e = gemm_run(d, ws, ws_n, st, cnt);
+  for (int i = 0; e == hipSuccess && i < iters; ++i) e = gemm_run(d, ws, ws_n, st);
   if (e == hipSuccess) e = hipEventRecord(t1, st);
   if (e == hipSuccess) e = hipEventSynchronize(t1);
   float ms = 0.f;
@@ -1192,7 +1182,6 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   for (float* p : {A, Bm, Cm, ws, aux, rowpart}) if (p) (void)hipFree(p);
   if (planes) (void)hipFree(planes);
   if (cpl) (void)hipFree(cpl);
-  if (cnt) (void)hipFree(cnt);
   if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
   return MVAE_OK;
 }

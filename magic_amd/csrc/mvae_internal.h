@@ -64,10 +64,6 @@ struct GemmDesc {
   int prec = GEMM_F32;                 // GemmPrec
   int variant = 0;                     // kernel variant (diagnostics / A-B); 0 = default
   int split = 0;                       // forced split-K (0 = planner)
-  // split-K combine of the 256x256 bf16-plane kernel: 1 = in the launch (every K-slice
-  // workgroup stores its fp32 partial write-through, the tile's last-arriving workgroup sums
-  // the slices in slice order and runs the epilogue); 0 = raw slabs + a reduction kernel
-  int fixup = 1;
   GemmEpi epi;
 };
 
@@ -75,11 +71,8 @@ struct GemmDesc {
 int gemm_plan_split(const GemmDesc& d, size_t max_ws);
 // Workspace elements (floats) the GEMM needs for its split-K slabs.
 size_t gemm_workspace_elems(const GemmDesc& d);
-// Launch. ws: device workspace of >= gemm_workspace_elems(d) floats; cnt: >= GEMM_MAX_TILES
-// zero-initialised ints (split-K tile tickets; every launch leaves them zero), private to the
-// stream (concurrent GEMMs need their own ws and cnt).
-constexpr int GEMM_MAX_TILES = 1 << 16;
-hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t st, int* cnt = nullptr);
+// Launch. ws: device workspace of >= gemm_workspace_elems(d) floats.
+hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t st);
 namespace gemm { struct Params; }
 hipError_t gemm_bf16_launch(const gemm::Params& p, const GemmDesc& d, int epi, hipStream_t st);
 // bf16-plane GEMMs: the 256x256 wide kernel serves d? (shape/alignment), and its split-K plan

@@ -303,45 +303,3 @@ def test_side_stream_schedule_is_bitwise_identical(prec):
         np.testing.assert_array_equal(parts, eng.grads.cpu().numpy())
     finally:
         eng.close()
-
-
-# ------------------------------------------------------------------ split-K in-launch combine
-@pytest.mark.parametrize("prec", [2, 1], ids=["f32x", "bf16"])
-@pytest.mark.parametrize("split", [2, 3, 4])
-@pytest.mark.parametrize("epi,act", [(0, 0), (1, 0), (2, 1), (4, 0)])
-@pytest.mark.parametrize("M,N,K,at,bt", [(600, 520, 1500, 0, 0), (513, 260, 1300, 1, 0),
-                                         (300, 700, 999, 0, 1)])
-def test_splitk_fixup_matches_reduction_kernel(prec, split, epi, act, M, N, K, at, bt):
-    """Forced split-K on the 256x256 kernel: the in-launch combine (last-arriving K-slice sums
-    the write-through slice partials in slice order) equals the separate reduction kernel
-    bitwise and float64 within the arithmetic's bound, for every epilogue and layout."""
-    lib = _lib.load()
-    g = torch.Generator(device="cuda").manual_seed(M + N + K + split)
-
-    def padded(r, c):
-        buf = torch.zeros(r, (c + 7) // 8 * 8, device="cuda")
-        buf[:, :c] = torch.randn(r, c, device="cuda", generator=g) * 0.3
-        return buf
-    A = padded(K, M) if at else padded(M, K)
-    Bm = padded(N, K) if bt else padded(K, N)
-    ld_aux = (N + 7) // 8 * 8
-    aux = torch.tanh(torch.randn(M, ld_aux, device="cuda", generator=g))
-    outs = []
-    for fix_off in (0, 1):
-        C = torch.full((M, N), float("nan"), device="cuda")
-        code = epi | (prec << 4) | (3 << 8) | (fix_off << 12) | (split << 13)
-        rc = lib.mvae_debug_gemm(M, N, K, A.data_ptr(), A.shape[1], at, Bm.data_ptr(), Bm.shape[1], bt,
-                                 C.data_ptr(), N, code, act, aux.data_ptr(), ld_aux,
-                                 torch.cuda.current_stream().cuda_stream)
-        assert rc == 0, lib.mvae_last_error(None)
-        outs.append(C)
-    assert torch.equal(outs[0], outs[1])
-    Ad = A[:, :M].double().T if at else A[:, :K].double()
-    Bd = Bm[:, :K].double().T if bt else Bm[:, :N].double()
-    acc = Ad @ Bd
-    a = aux[:, :N].double()
-    ref = {0: acc, 1: torch.tanh(acc), 2: torch.where(a < 0, acc * (a + 1), acc),
-           4: torch.sigmoid(acc)}[epi]
-    mag = (Ad.abs() @ Bd.abs()).max().item()
-    bound = (2e-6 if prec == 2 else 1e-2) * mag + 1e-6
-    assert (outs[0].double() - ref).abs().max().item() <= bound

@@ -12,5 +12,9 @@ for spec in "$@"; do
   echo "[gpu_steps] $(date +%T) $name rc=$rc"
   tail -4 "gpurun_out/$name.log"
   if [ $rc -ge 2 ]; then echo "[gpu_steps] stopping after $name (rc=$rc)"; exit $rc; fi
+  # a GPU fault reported as an ordinary Python error (rc 1) also ends the call
+  if grep -qE "illegal memory access|Memory access fault|HSA_STATUS_ERROR|hipErrorLaunchFailure|page fault" "gpurun_out/$name.log"; then
+    echo "[gpu_steps] GPU fault in $name: stopping"; exit 3
+  fi
 done
 echo "[gpu_steps] done"
