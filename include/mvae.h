@@ -189,7 +189,7 @@ int mvae_timing_reset(mvae_ctx* ctx);
  * (at=0) or [K][M] (at=1), B stored [K][N] (bt=0) or [N][K] (bt=1). epi: 0 store,
  * 1 act (act: 0 tanh, 1 elu), 2 C = acc * act'(aux), 4 sigmoid; epi | (prec << 4) |
  * (variant << 8) selects the arithmetic (MVAE_PREC_*) and kernel (0 auto, 3 the 256x256
- * bf16 kernel, 4 the 128x128 one). Workspace is allocated and freed inside
+ * bf16 kernel, 4 the 128x128 one, 9 the fp32 VALU kernel for skinny shapes). Workspace is allocated and freed inside
  * (synchronous; tests only). mvae_bench_gemm: variant | (prec << 4) | (epi << 8).    */
 int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, int variant, int iters,
                     void* stream, float* avg_ms);

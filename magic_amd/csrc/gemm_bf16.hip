@@ -49,6 +49,8 @@ struct PParams {
   unsigned char pa[6], pb[6];
   int pab;                          // pa[i] | pb[i] << 2 packed 4 bits per pair (no memory reads)
   const int* dyn;                   // A residual planes nonzero? (nullptr: use all pairs)
+  int diag;                         // timing diagnostics: bit 0 = no operand copies after the
+                                    // prologue (the k-loop multiplies stale LDS images)
 };
 
 template <bool KC, int BK>
@@ -482,11 +484,12 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16r_kernel(PParams pp) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     // B copy for it+1 (needed first), A copy for it+2 (after the first k16-step)
-    const bool nb1 = it + 1 < total && (kt1 != kt0 || pb_of(pr1) != pb_of(pr0));
+    const bool dma = !(pp.diag & 1);
+    const bool nb1 = dma && it + 1 < total && (kt1 != kt0 || pb_of(pr1) != pb_of(pr0));
     const int sb1 = nb1 ? sb0 ^ 1 : sb0;
     if (nb1) lb.issue(Bm + pb_of(pr1) * pp.pB, p.ldb, t.ks + kt1 * BK, t.ke,
                       smem + (3 + sb1) * IMG, wave);
-    const bool na2 = it + 2 < total && (kt2 != kt1 || pa_of(pr2) != pa_of(pr1));
+    const bool na2 = dma && it + 2 < total && (kt2 != kt1 || pa_of(pr2) != pa_of(pr1));
     sa2 = na2 ? (sa1 == 2 ? 0 : sa1 + 1) : sa1;
     const short* sa = smem + sa0 * IMG;
     const short* sb = smem + (3 + sb0) * IMG;
@@ -650,6 +653,7 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   p.A = d.Ap; p.pA = d.pA;
   p.B = d.Bp; p.pB = d.pB;
   p.dyn = d.dynA;
+  p.diag = d.diag;
   // plane pairs (i, j), i + j < max(nA, nB); the pairs with i = 0 first
   int n = 0;
   const int T = d.nA > d.nB ? d.nA : d.nB;

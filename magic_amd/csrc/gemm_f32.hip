@@ -319,6 +319,7 @@ int gemm_bce_nblk(int N) { return (N + BN - 1) / BN; }
 
 int gemm_plan_split(const GemmDesc& d, size_t max_ws) {
   if (d.epi.mode == EPI_BCE || d.epi.mode == EPI_BCEB || d.epi.mode == EPI_SIGMOID) return 1;
+  if (d.valu) return gemm_valu_split(d, max_ws);
   if (gemm_bf16_wide(d)) return gemm_bf16_wide_split(d, max_ws);
   const int ntm = (d.M + BM - 1) / BM, ntn = (d.N + BN - 1) / BN;
   const long long tiles = (long long)ntm * ntn * d.batch;
@@ -364,6 +365,7 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   p.kchunk = ((ktiles + split - 1) / split) * kb;
   if (split == 1) {
     p.C = d.C; p.ldc = d.ldc; p.sC = d.sC;
+    if (d.valu) return gemm_valu_launch(p, d, d.epi.mode, st);
     if (d.prec != GEMM_F32) {
       // BCE with a bf16-plane target: two launches, each running only for its *xdyn state
       if (d.epi.mode == EPI_BCE && d.epi.xp && d.epi.xdyn) {
@@ -387,13 +389,16 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   p.C = ws; p.ldc = d.N; p.sC = (long long)d.M * d.N;
   p.epi.cp = nullptr;  // planes (and the fp32 output, if any) are written by the reduction
   p.epi.c32 = 1;       // the slabs themselves always
-  hipError_t err = d.prec != GEMM_F32 ? gemm_bf16_launch(p, d, EPI_STORE, st)
+  hipError_t err = d.valu ? gemm_valu_launch(p, d, EPI_STORE, st)
+                 : d.prec != GEMM_F32 ? gemm_bf16_launch(p, d, EPI_STORE, st)
                                       : launch_store(p, d.at, d.bt, d.variant, st);
   if (err != hipSuccess) return err;
   const long long total = (long long)d.M * d.N;
   int grid = (int)std::min<long long>((total + 255) / 256, 2048);
   dim3 g(grid, 1, d.batch);
-  if (splitk_reduce4_ok(d)) {
+  // small outputs (weight gradients of the latent head / decoder layer 1): one element per
+  // thread, so the slices' loads spread over more waves
+  if (splitk_reduce4_ok(d) && total >= (1 << 18)) {
     dim3 g4((int)std::min<long long>((total / 4 + 255) / 256, 2048), 1, d.batch);
     switch (d.epi.mode) {
       case EPI_STORE:

@@ -71,6 +71,7 @@ struct mvae_ctx {
   size_t sync_next = 0;
   bool use_side = true;      // option "side_stream"
   bool side_pending = false; // side stream holds work the caller's stream has not joined
+  bool valu = true;          // skinny GEMMs on the fp32 VALU kernel (env MVAE_NO_VALU=1: off)
   std::vector<void*> allocs;
   // bf16 plane images (bf16 / f32x modes): fp32 buffer -> planes of the same layout
   struct PlaneBuf { float* base; size_t n; Planes pl; };
@@ -445,6 +446,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     return (int)e;
   }
   build_schedule(c);
+  if (const char* nv = std::getenv("MVAE_NO_VALU"); nv && *nv == '1') c->valu = false;
   const int gp = cfg->precision == MVAE_PREC_BF16 ? GEMM_BF16
                  : (cfg->precision == MVAE_PREC_F32X ? GEMM_F32X : GEMM_F32);
   c->np = gp == GEMM_BF16 ? 1 : (gp == GEMM_F32X ? 3 : 0);
@@ -482,6 +484,14 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   }
   auto wire = [&](GemmDesc& d) {
     d.prec = gp;
+    // skinny products (an output dimension or K <= 64 and no 256x256 plane-kernel shape: the
+    // latent head and the decoder's first layer at small L) run on the fp32 VALU kernel
+    const long long t256 = (long long)((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
+    const bool wide_shape = d.M >= 256 && d.N >= 256 && !(d.K <= 64 && t256 < 256);
+    if (c->valu && gemm_valu_fits(d) && !(gp != GEMM_F32 && wide_shape)) {
+      d.prec = GEMM_F32;
+      d.valu = 1;
+    }
     if (!c->np) return;
     const Planes a = planes_of(c, d.A), b = planes_of(c, d.B), o = planes_of(c, d.C);
     d.Ap = a.p; d.pA = a.stride; d.nA = c->np;
@@ -1022,6 +1032,7 @@ extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int
   GemmDesc d = gd(M, N, K, A, lda, at != 0, Bm, ldb, bt != 0, Cm, ldc, epi & 15);
   d.prec = (epi >> 4) & 15;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
   d.variant = (epi >> 8) & 15;
+  if (d.variant == 9) { d.valu = 1; d.prec = GEMM_F32; d.variant = 0; }  // the fp32 VALU kernel
   d.epi.act = act;
   d.epi.aux = aux;
   d.epi.ld_aux = ld_aux;
@@ -1127,6 +1138,8 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   d.batch = batch; d.sA = (long long)sa; d.sB = (long long)sb; d.sC = (long long)M * N;
   d.variant = variant & 15;
   d.prec = (variant >> 4) & 15;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
+  if (d.variant == 9) { d.valu = 1; d.prec = GEMM_F32; d.variant = 0; }  // the fp32 VALU kernel
+  d.diag = (variant >> 12) & 15; // kernel timing diagnostics (results meaningless)
   unsigned short* planes = nullptr;
   const int np = d.prec == GEMM_F32 ? 0 : (d.prec == GEMM_BF16 ? 1 : 3);
   hipError_t e = hipMalloc(&A, na * 4);

@@ -64,6 +64,8 @@ struct GemmDesc {
   int prec = GEMM_F32;                 // GemmPrec
   int variant = 0;                     // kernel variant (diagnostics / A-B); 0 = default
   int split = 0;                       // forced split-K (0 = planner)
+  int diag = 0;                        // kernel timing diagnostics (gemm_bf16.hip PParams::diag)
+  int valu = 0;                        // 1: the fp32 VALU kernel (gemm_valu.hip; skinny shapes)
   GemmEpi epi;
 };
 
@@ -77,6 +79,10 @@ namespace gemm { struct Params; }
 hipError_t gemm_bf16_launch(const gemm::Params& p, const GemmDesc& d, int epi, hipStream_t st);
 // bf16-plane GEMMs: the 256x256 wide kernel serves d? (shape/alignment), and its split-K plan
 bool gemm_bf16_wide(const GemmDesc& d);
+// fp32 VALU kernel for skinny products (an output dimension or K <= 64)
+bool gemm_valu_fits(const GemmDesc& d);
+int gemm_valu_split(const GemmDesc& d, size_t max_ws);
+hipError_t gemm_valu_launch(const gemm::Params& p, const GemmDesc& d, int epi, hipStream_t st);
 int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws);
 // Number of column blocks the BCE epilogue writes per row (rowpart's inner dim).
 int gemm_bce_nblk(int N);

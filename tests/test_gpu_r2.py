@@ -303,3 +303,50 @@ def test_side_stream_schedule_is_bitwise_identical(prec):
         np.testing.assert_array_equal(parts, eng.grads.cpu().numpy())
     finally:
         eng.close()
+
+
+# ------------------------------------------------------------------ fp32 VALU kernel (skinny GEMMs)
+@pytest.mark.parametrize("at,bt", [(0, 0), (1, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(1, 1, 1), (37, 53, 29), (12288, 40, 501), (21, 500, 4096),
+                                   (4096, 20, 500), (16384, 500, 40), (501, 40, 8192), (70, 130, 65)])
+def test_gemm_valu_layouts(at, bt, M, N, K):
+    """The skinny-shape fp32 VALU kernel (variant 9) on every layout and the step's skinny
+    shapes at L = 20 (head forward / weight gradient, decoder layer 1 and its gradients, the
+    latent-head dgrad), incl. its split-K, against float64 at the fp32 bound."""
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(M * 3 + N * 7 + K)
+    A = torch.randn((K, M) if at else (M, K), device="cuda", generator=g)
+    Bm = torch.randn((N, K) if bt else (K, N), device="cuda", generator=g)
+    C = torch.full((M, N), float("nan"), device="cuda")
+    rc = lib.mvae_debug_gemm(M, N, K, A.data_ptr(), A.shape[1], at, Bm.data_ptr(), Bm.shape[1], bt,
+                             C.data_ptr(), N, 9 << 8, 0, None, 0, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, lib.mvae_last_error(None)
+    Ad = A.double().T if at else A.double()
+    Bd = Bm.double().T if bt else Bm.double()
+    err = (C.double() - Ad @ Bd).abs().max().item()
+    mag = (Ad.abs() @ Bd.abs()).max().item()
+    assert err <= 2e-6 * mag + 1e-6, (err, mag)
+
+
+@pytest.mark.parametrize("epi,act", [(1, 0), (1, 1), (2, 0), (2, 1), (4, 0)])
+def test_gemm_valu_epilogues(epi, act):
+    lib = _lib.load()
+    M, N, K = 300, 500, 21
+    g = torch.Generator(device="cuda").manual_seed(11 + epi + act)
+    A = torch.randn(M, K, device="cuda", generator=g) * 0.3
+    Bm = torch.randn(K, N, device="cuda", generator=g) * 0.3
+    aux = torch.tanh(torch.randn(M, N, device="cuda", generator=g)) if act == 0 else \
+        torch.nn.functional.elu(torch.randn(M, N, device="cuda", generator=g))
+    C = torch.empty(M, N, device="cuda")
+    rc = lib.mvae_debug_gemm(M, N, K, A.data_ptr(), K, 0, Bm.data_ptr(), N, 0, C.data_ptr(), N,
+                             epi | (9 << 8), act, aux.data_ptr(), N, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, lib.mvae_last_error(None)
+    acc = A.double() @ Bm.double()
+    if epi == 1:
+        ref = torch.tanh(acc) if act == 0 else torch.where(acc < 0, torch.exp(acc) - 1, acc)
+    elif epi == 2:
+        a = aux.double()
+        ref = acc * (1 - a * a) if act == 0 else torch.where(a < 0, acc * (a + 1), acc)
+    else:
+        ref = torch.sigmoid(acc)
+    assert (C.double() - ref).abs().max().item() < 1e-5
