@@ -263,16 +263,20 @@ struct WLoad {
   }
   // LDS instructions per fragment
   static constexpr int NRD = KC ? 1 : 2;
-  // fragment (8 consecutive k) of the 32-row block at rb, k16-step ks. The transposing reads
-  // are inline asm: the builtin makes hipcc wait for every outstanding LDS-DMA (vmcnt(0))
-  // before it, serialising the next tile's copy with this tile's MFMAs. Their results are
-  // waited for explicitly (wait_lds) before use.
+  // fragment (8 consecutive k) of the 32-row block at rb, k16-step ks. All fragment reads are
+  // inline asm and their results are waited for explicitly (wait_lds) before use: the
+  // transposing-read builtin makes hipcc wait for every outstanding LDS-DMA (vmcnt(0)), and a
+  // compiler-visible ds_read_b128 next to the asm reads makes it wait lgkmcnt(0) before the
+  // first use, which also waits for the NEXT k16-step's prefetched fragments (measured: the
+  // MFMA-only loop then ran at ~47 % of peak).
   __device__ __forceinline__ bf16x8 frag(const short* s, unsigned s_lds, int rb, int ks,
                                          int lane) const {
     if constexpr (KC) {
       const int row = rb + (lane & 31);
       const int pos = (2 * ks + (lane >> 5)) ^ swz(row);
-      const s16x8 v = *reinterpret_cast<const s16x8*>(s + row * BK + pos * 8);
+      const unsigned a = s_lds + 2u * (unsigned)(row * BK + pos * 8);
+      s16x8 v;
+      asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
       return __builtin_bit_cast(bf16x8, v);
     } else {
       const int i = lane & 15, q = i >> 2, pp = i & 3;
@@ -533,6 +537,195 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16r_kernel(PParams pp) {
   epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
 }
 
+// ---------------------------------------------------------------------------------------
+// Interleaved ring kernel (the default wide kernel): the operand rings, tile and epilogue of
+// gemm_bf16r_kernel, with the LDS fragment reads of the NEXT k16-step issued between the
+// MFMAs of the current one (one fragment per MFMA gap, cdna MI355X_MICROARCH.md §LDS: up to
+// three reads per 32x32x16 gap are free), so no k16-step waits for its reads and no read
+// burst stalls the MFMA issue. The iteration hand-off sits inside the last k16-step: once the
+// step's fragments are in registers every read of the iteration's images is done, so after
+// four of its MFMAs the waves wait for the next iteration's images (counted vmcnt), pass one
+// raw s_barrier, issue the copies into the slots the iteration freed, and read the next
+// iteration's first fragments behind the remaining four MFMAs.
+// Copies: B image of it+2 and A image of it+3 are issued in iteration it (B ring 2 slots,
+// A ring 3 slots), each only when the (plane, k-tile) changes.
+template <bool AT, bool BT, int EPI>
+__global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
+  constexpr int BK = 64;
+  constexpr int IMG = WT * BK;  // bf16 elements per operand image
+  constexpr int KS = BK / 16;
+  const Params& p = pp.g;
+  if (epi_skip<EPI>(p.epi)) return;
+  __shared__ __attribute__((aligned(16))) short smem[5 * IMG];  // A slots 0-2 | B slots 0-1
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const Tile t = tile_of_t<WT, WT>(p, true);
+  const unsigned short* __restrict__ A = pp.A + t.bi * p.sA;
+  const unsigned short* __restrict__ Bm = pp.B + t.bi * p.sB;
+
+  WLoad<!AT, BK> la;
+  WLoad<BT, BK> lb;
+  la.init(p.lda, t.m0, p.M, wave, lane);
+  lb.init(p.ldb, t.n0, p.N, wave, lane);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int np = (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
+  const int nkt = t.ks < t.ke ? (t.ke - t.ks + BK - 1) / BK : 0;
+  const int total = np * nkt;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
+  auto pa_of = [&](int pr) { return (pp.pab >> (4 * pr)) & 3; };
+  auto pb_of = [&](int pr) { return (pp.pab >> (4 * pr + 2)) & 3; };
+  auto adv = [&](int& kt, int& pr) { if (++pr == np) { pr = 0; ++kt; } };
+  // A cursor: iteration ia (k-tile, pair) of the last A image issued, its slot; B likewise
+  int akt = 0, apr = 0, ia = 0, asl = 0;
+  int bkt = 0, bpr = 0, ib = 0, bsl = 0;
+  bool pend_a = false;  // the A copy issued with the last B copy (vmcnt accounting)
+  // issue the A image of iteration ia+1 if it differs from ia's (and exists)
+  auto next_a = [&]() -> bool {
+    if (ia + 1 >= total) return false;
+    const int k0 = akt, p0 = apr;
+    adv(akt, apr);
+    ++ia;
+    if (akt == k0 && pa_of(apr) == pa_of(p0)) return false;
+    asl = asl == 2 ? 0 : asl + 1;
+    la.issue(A + pa_of(apr) * pp.pA, p.lda, t.ks + akt * BK, t.ke, smem + asl * IMG, wave);
+    return true;
+  };
+  auto next_b = [&]() -> bool {
+    if (ib + 1 >= total) return false;
+    const int k0 = bkt, p0 = bpr;
+    adv(bkt, bpr);
+    ++ib;
+    if (bkt == k0 && pb_of(bpr) == pb_of(p0)) return false;
+    bsl ^= 1;
+    lb.issue(Bm + pb_of(bpr) * pp.pB, p.ldb, t.ks + bkt * BK, t.ke, smem + (3 + bsl) * IMG, wave);
+    return true;
+  };
+  // slots of the images of iterations it .. it+2 (A) and it .. it+1 (B)
+  int sa_q[3] = {0, 0, 0};
+  int sb_q[2] = {0, 0};
+
+  bf16x8 fa[2][4], fb[2][2];
+  auto rd_a = [&](int slot, int ks, int mi, bf16x8& a) {
+    a = la.frag(smem + slot * IMG, lds0 + 2u * (unsigned)(slot * IMG), wm * 128 + mi * 32, ks, lane);
+  };
+  auto rd_b = [&](int slot, int ks, int ni, bf16x8& b) {
+    b = lb.frag(smem + (3 + slot) * IMG, lds0 + 2u * (unsigned)((3 + slot) * IMG),
+                wn * 64 + ni * 32, ks, lane);
+  };
+
+  if (total > 0) {
+    // prologue: A(0), B(0), A(1); wait for A(0), B(0); barrier; B(1), A(2)
+    la.issue(A + pa_of(0) * pp.pA, p.lda, t.ks, t.ke, smem, wave);
+    lb.issue(Bm + pb_of(0) * pp.pB, p.ldb, t.ks, t.ke, smem + 3 * IMG, wave);
+    const bool a1 = next_a();
+    sa_q[0] = 0; sa_q[1] = asl;
+    if (a1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    next_b();
+    sb_q[0] = 0; sb_q[1] = bsl;
+    pend_a = next_a();
+    sa_q[2] = asl;
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni) rd_b(sb_q[0], 0, ni, fb[0][ni]);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) rd_a(sa_q[0], 0, mi, fa[0][mi]);
+  }
+  for (int it = 0; it < total; ++it) {
+    const int sa = sa_q[0], sb = sb_q[0];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      const int cur = ks & 1, nx = cur ^ 1;
+      wait_lds<0>();  // this step's fragments (read during the previous step's MFMAs)
+      __builtin_amdgcn_sched_barrier(0);
+      if (ks + 1 < KS) {
+        // MFMA i, then one fragment of step ks+1 in its gap
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int mi = i >> 1, ni = i & 1;
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][mi], fb[cur][ni], acc[mi][ni], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (i < 2) rd_b(sb, ks + 1, i, fb[nx][i]);
+          else if (i < 6) rd_a(sa, ks + 1, i - 2, fa[nx][i - 2]);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int mi = i >> 1, ni = i & 1;
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][mi], fb[cur][ni], acc[mi][ni], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+        const bool more = it + 1 < total;
+        if (more) {
+          // images of it+1 landed (only the A copy issued after its B copy may be in flight),
+          // every wave's reads of it's images are done: its freed slots can be refilled
+          if (pend_a) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          __builtin_amdgcn_s_barrier();
+          asm volatile("" ::: "memory");
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 4; i < 8; ++i) {
+          const int mi = i >> 1, ni = i & 1;
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][mi], fb[cur][ni], acc[mi][ni], 0, 0, 0);
+          __builtin_amdgcn_sched_barrier(0);
+          if (more) {
+            if (i == 4) {
+              // fragments of it+1's first step (its images: slot queues shifted below)
+#pragma unroll
+              for (int n2 = 0; n2 < 2; ++n2) rd_b(sb_q[1], 0, n2, fb[nx][n2]);
+              rd_a(sa_q[1], 0, 0, fa[nx][0]);
+            } else if (i == 5) {
+              rd_a(sa_q[1], 0, 1, fa[nx][1]);
+              rd_a(sa_q[1], 0, 2, fa[nx][2]);
+            } else if (i == 6) {
+              rd_a(sa_q[1], 0, 3, fa[nx][3]);
+              // copies into the freed slots: B of it+2, A of it+3
+              next_b();
+              sb_q[0] = sb_q[1]; sb_q[1] = bsl;
+              pend_a = next_a();
+              sa_q[0] = sa_q[1]; sa_q[1] = sa_q[2]; sa_q[2] = asl;
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+    }
+    // KS is even: the next iteration's step 0 reads land in fa/fb[0]
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
+}
+
+template <bool AT, bool BT, int EPI>
+hipError_t launch_q(const PParams& p, hipStream_t st) {
+  const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
+  hipLaunchKernelGGL((gemm_bf16q_kernel<AT, BT, EPI>), dim3(nwg), dim3(WNT), 0, st, p);
+  return hipGetLastError();
+}
+
+template <int EPI>
+hipError_t launch_q_t(const PParams& p, bool at, bool bt, hipStream_t st) {
+  if (!at && !bt) return launch_q<false, false, EPI>(p, st);
+  if (at && !bt) return launch_q<true, false, EPI>(p, st);
+  if (!at && bt) return launch_q<false, true, EPI>(p, st);
+  return launch_q<true, true, EPI>(p, st);
+}
+
 template <bool AT, bool BT, int EPI, bool SP>
 hipError_t launch_r(const PParams& p, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
@@ -564,7 +757,8 @@ hipError_t launch_wide_t(const PParams& p, bool at, bool bt, hipStream_t st) {
 }
 
 // wide variants (diagnostics, EPI_STORE): 5 = two-stage form at BK 32 x 4 stages, 7 = ring form
-// with s_setprio, 8 = two-stage form at BK 64 x 2 stages; otherwise (0, 3, 6) the ring form
+// with s_setprio, 8 = two-stage form at BK 64 x 2 stages; 6 = ring form (any epilogue);
+// otherwise (0, 3) the interleaved ring form
 template <int EPI>
 hipError_t launch_wide(const PParams& p, bool at, bool bt, int variant, hipStream_t st) {
   if constexpr (EPI == EPI_STORE) {
@@ -572,9 +766,11 @@ hipError_t launch_wide(const PParams& p, bool at, bool bt, int variant, hipStrea
     if (variant == 7) return launch_ring_t<EPI, true>(p, at, bt, st);
     if (variant == 8) return launch_wide_t<EPI, 64, 2>(p, at, bt, st);
   }
-  // default: the ring form (profiles/r1/gemm_ab_ring.txt: +3..28 % over the two-stage form
-  // on the step's shapes; s_setprio around the MFMA clusters measured neutral)
-  return launch_ring_t<EPI, false>(p, at, bt, st);
+  // 6: the ring form of round 1 (profiles/r1/gemm_ab_ring.txt: +3..28 % over the two-stage
+  // form on the step's shapes; s_setprio around the MFMA clusters measured neutral)
+  if (variant == 6) return launch_ring_t<EPI, false>(p, at, bt, st);
+  // default: the interleaved ring form
+  return launch_q_t<EPI>(p, at, bt, st);
 }
 
 template <bool AT, bool BT, int EPI, int BK, bool DB>

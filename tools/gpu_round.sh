@@ -5,7 +5,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
 OUT=$R/gpurun_out
-TAG=${TAG:-r1}
+TAG=${TAG:-r2}
 mkdir -p $OUT
 step() {  # step <name> <timeout> <cmd...>
   local name=$1 t=$2; shift 2
@@ -16,7 +16,7 @@ step() {  # step <name> <timeout> <cmd...>
   return $rc
 }
 if [ -z "$SKIP_TESTS" ]; then
-  step tests 1200 python -m pytest tests -m gpu -q --timeout 900 -p no:cacheprovider > $OUT/tests_$TAG.log 2>&1
+  step tests 1100 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/tests_$TAG.log 2>&1
   rc=$?; tail -3 $OUT/tests_$TAG.log
   [ $rc -gt 1 ] && exit $rc
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.log 2>&1 || exit $?
