@@ -549,7 +549,7 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16r_kernel(PParams pp) {
 // iteration's first fragments behind the remaining four MFMAs.
 // Copies: B image of it+2 and A image of it+3 are issued in iteration it (B ring 2 slots,
 // A ring 3 slots), each only when the (plane, k-tile) changes.
-template <bool AT, bool BT, int EPI>
+template <bool AT, bool BT, int EPI, bool TE>
 __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   constexpr int BK = 64;
   constexpr int IMG = WT * BK;  // bf16 elements per operand image
@@ -708,22 +708,23 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
+  if constexpr (TE) epilogue_wide<EPI>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
+  else epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
 }
 
-template <bool AT, bool BT, int EPI>
+template <bool AT, bool BT, int EPI, bool TE>
 hipError_t launch_q(const PParams& p, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
-  hipLaunchKernelGGL((gemm_bf16q_kernel<AT, BT, EPI>), dim3(nwg), dim3(WNT), 0, st, p);
+  hipLaunchKernelGGL((gemm_bf16q_kernel<AT, BT, EPI, TE>), dim3(nwg), dim3(WNT), 0, st, p);
   return hipGetLastError();
 }
 
-template <int EPI>
+template <int EPI, bool TE>
 hipError_t launch_q_t(const PParams& p, bool at, bool bt, hipStream_t st) {
-  if (!at && !bt) return launch_q<false, false, EPI>(p, st);
-  if (at && !bt) return launch_q<true, false, EPI>(p, st);
-  if (!at && bt) return launch_q<false, true, EPI>(p, st);
-  return launch_q<true, true, EPI>(p, st);
+  if (!at && !bt) return launch_q<false, false, EPI, TE>(p, st);
+  if (at && !bt) return launch_q<true, false, EPI, TE>(p, st);
+  if (!at && bt) return launch_q<false, true, EPI, TE>(p, st);
+  return launch_q<true, true, EPI, TE>(p, st);
 }
 
 template <bool AT, bool BT, int EPI, bool SP>
@@ -756,6 +757,22 @@ hipError_t launch_wide_t(const PParams& p, bool at, bool bt, hipStream_t st) {
   return launch_w<true, true, EPI, BK, DEPTH>(p, st);
 }
 
+// the row-major 16-B epilogue (epilogue_wide) applies: bases and strides keep every 8-column
+// chunk of every operand it touches 16-B aligned
+bool wide_epi_vec_ok(const Params& g) {
+  auto al = [](const void* q) { return (reinterpret_cast<uintptr_t>(q) & 15) == 0; };
+  const GemmEpi& e = g.epi;
+  if (e.c32 && (!al(g.C) || (g.ldc & 3) || (g.sC & 3))) return false;
+  if (e.cp && (!al(e.cp) || (g.ldc & 7) || (g.sC & 7) || (e.pc & 7))) return false;
+  if (e.mode == EPI_DACT && (!al(e.aux) || (e.ld_aux & 3))) return false;
+  if (e.mode == EPI_BCE || e.mode == EPI_BCEB) {
+    if (e.x && (!al(e.x) || (e.ldx & 3))) return false;
+    if (e.xp && (!al(e.xp) || (e.ldx & 7))) return false;
+    if (e.y && (!al(e.y) || (e.ldy & 3))) return false;
+  }
+  return true;
+}
+
 // wide variants (diagnostics, EPI_STORE): 5 = two-stage form at BK 32 x 4 stages, 7 = ring form
 // with s_setprio, 8 = two-stage form at BK 64 x 2 stages; 6 = ring form (any epilogue);
 // otherwise (0, 3) the interleaved ring form
@@ -769,8 +786,14 @@ hipError_t launch_wide(const PParams& p, bool at, bool bt, int variant, hipStrea
   // 6: the ring form of round 1 (profiles/r1/gemm_ab_ring.txt: +3..28 % over the two-stage
   // form on the step's shapes; s_setprio around the MFMA clusters measured neutral)
   if (variant == 6) return launch_ring_t<EPI, false>(p, at, bt, st);
-  // default: the interleaved ring form
-  return launch_q_t<EPI>(p, at, bt, st);
+  // default: the interleaved ring form; its epilogue goes through LDS (row-major 16-B stores)
+  // when the tile writes bf16 planes or is the BCE head (2-B plane stores and 4-B target loads
+  // per element otherwise), and stays in the C/D layout for fp32-only outputs (split-K slabs:
+  // 128-B row segments already, where the LDS round trip measured 5-10 % slower)
+  constexpr bool BCE = EPI == EPI_BCE || EPI == EPI_BCEB;
+  if ((p.g.epi.cp || BCE) && variant != 10 && wide_epi_vec_ok(p.g))
+    return launch_q_t<EPI, true>(p, at, bt, st);
+  return launch_q_t<EPI, false>(p, at, bt, st);
 }
 
 template <bool AT, bool BT, int EPI, int BK, bool DB>

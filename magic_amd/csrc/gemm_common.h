@@ -196,6 +196,156 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
   }
 }
 
+// Row-major epilogue of the 256x256 wide kernels (8 waves 2x4, each 4x2 32x32 accumulators).
+// The C/D layout puts 32 consecutive columns of one row in a half-wave, so a direct store is one
+// 2-B (bf16 plane) or 4-B element per lane: a 256x256 tile with three output planes takes 384
+// store instructions per thread, and the BCE target/aux loads are as narrow. Here each 64-row
+// band (accumulator row block mi of both wave rows) goes through LDS instead: the waves write
+// their raw accumulators row-major ([64][256] fp32, 64 KB, two bands in flight), pass a barrier,
+// and every thread then owns 8 consecutive columns of 4 rows: 16-B loads of the epilogue's
+// operands (DACT aux, BCE target), the math, and 16-B stores of the fp32 output and of each
+// bf16 plane. BCE row partials: each 8-column chunk's terms summed in order, then a fixed xor
+// tree over the 16 lanes of a 128-column block; lane 0 of the 16 writes rowpart. Requires
+// (wide_epi_vec_ok) 16-B aligned bases and ld / plane / batch strides that keep 8-column chunks
+// 16-B aligned; chunks that cross N fall back to element stores.
+__device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8f(float* p, const float (&v)[8]) {
+  *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ unsigned short bf16_rn_bits(float v) {
+  return __builtin_bit_cast(unsigned short, __float2bfloat16(v));
+}
+// 8 values -> n bf16 planes, one 16-B store per plane (exact split for n = 3)
+__device__ __forceinline__ void st8_planes(unsigned short* cp, long long pc, int n, size_t o,
+                                           const float (&v)[8]) {
+  float r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = v[j];
+  for (int t = 0; t < n; ++t) {
+    unsigned w[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const unsigned short lo = bf16_rn_bits(r[2 * j]), hi = bf16_rn_bits(r[2 * j + 1]);
+      r[2 * j] -= bf16_bits_to_f32(lo);
+      r[2 * j + 1] -= bf16_bits_to_f32(hi);
+      w[j] = (unsigned)lo | (unsigned)hi << 16;
+    }
+    *reinterpret_cast<uint4*>(cp + t * pc + o) = make_uint4(w[0], w[1], w[2], w[3]);
+  }
+}
+
+template <int EPI>
+__device__ __forceinline__ void epilogue_wide(const Params& p, const Tile& t, f32x16 (&acc)[4][2],
+                                              float* lds, int wm, int wn) {
+  constexpr int TW = 256, BAND = 64 * TW;  // floats per band buffer
+  constexpr bool BCE = EPI == EPI_BCE || EPI == EPI_BCEB;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const GemmEpi& e = p.epi;
+  float* __restrict__ C = p.C + (size_t)t.z * p.sC;
+  unsigned short* __restrict__ cp = e.cp ? e.cp + (size_t)t.z * p.sC : nullptr;
+  const int c8 = tid & 31, rr = tid >> 5;   // reader: chunk of 8 columns, row within 16
+  const int col0 = t.n0 + 8 * c8;
+  const int nblk = (p.N + 127) / 128;
+  const int gb = t.nt * 2 + (c8 >> 4);      // 128-column block of this chunk
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    float* band = lds + (mi & 1) * BAND;
+    // writer: this wave's 32 x 64 block of the band, C/D layout -> row-major
+#pragma unroll
+    for (int ni = 0; ni < 2; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        band[row * TW + wn * 64 + ni * 32 + (lane & 31)] = acc[mi][ni][r];
+      }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int br = rr + 16 * q;                               // band row
+      const int row = t.m0 + (br >> 5) * 128 + mi * 32 + (br & 31);  // tile row -> global
+      float v[8];
+      const float4 a = *reinterpret_cast<const float4*>(band + br * TW + 8 * c8);
+      const float4 b = *reinterpret_cast<const float4*>(band + br * TW + 8 * c8 + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      const bool rok = row < p.M;
+      const bool full = rok && col0 + 8 <= p.N;
+      const int nv = !rok ? 0 : (col0 >= p.N ? 0 : (p.N - col0 < 8 ? p.N - col0 : 8));
+      float rs = 0.f;
+      if (nv > 0) {
+        float sv[8];
+        if constexpr (EPI == EPI_DACT) {
+          const int ar = row >= e.remap_split ? row - e.remap_shift : row;
+          const float* src = e.aux + (size_t)ar * e.ld_aux + col0;
+          if (full) ld8f(src, sv);
+          else
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sv[j] = j < nv ? src[j] : 0.f;
+        }
+        if constexpr (EPI == EPI_BCE) {
+          const float* src = e.x + (size_t)row * e.ldx + col0;
+          if (full) ld8f(src, sv);
+          else
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sv[j] = j < nv ? src[j] : 0.f;
+        }
+        if constexpr (EPI == EPI_BCEB) {
+          const unsigned short* src = e.xp + (size_t)row * e.ldx + col0;
+          if (full) {
+            const uint4 w = *reinterpret_cast<const uint4*>(src);
+            const unsigned ww[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              sv[2 * j] = __uint_as_float(ww[j] << 16);
+              sv[2 * j + 1] = __uint_as_float(ww[j] & 0xffff0000u);
+            }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sv[j] = j < nv ? bf16_bits_to_f32(src[j]) : 0.f;
+          }
+        }
+        float yv[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          if constexpr (BCE) {
+            yv[j] = sigmoid_fast(v[j]);
+            // -log(y^x (1-y)^(1-x)) with TF pow(0,0) = 1 (no epsilon), 11a/vae.py:266-269
+            if (j < nv) rs += bce_term(yv[j], sv[j]);
+            v[j] = (yv[j] - sv[j]) * e.scale;
+          }
+          if constexpr (EPI == EPI_ACT) v[j] = act_f(v[j], e.act);
+          if constexpr (EPI == EPI_SIGMOID) v[j] = sigmoid_f(v[j]);
+          if constexpr (EPI == EPI_DACT) v[j] = dact_f(v[j], sv[j], e.act);
+        }
+        const size_t o = (size_t)row * p.ldc + col0;
+        if (full) {
+          if (e.c32) st8f(C + o, v);
+          if (cp) st8_planes(cp, e.pc, e.ncp, o, v);
+          if constexpr (BCE)
+            if (e.y) st8f(e.y + (size_t)row * e.ldy + col0, yv);
+        } else {
+          for (int j = 0; j < nv; ++j) {
+            if (e.c32) C[o + j] = v[j];
+            if (cp) store_planes(cp, e.pc, e.ncp, o + j, v[j]);
+            if constexpr (BCE)
+              if (e.y) e.y[(size_t)row * e.ldy + col0 + j] = yv[j];
+          }
+        }
+      }
+      if constexpr (BCE) {
+#pragma unroll
+        for (int off = 8; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
+        if ((c8 & 15) == 0 && rok && gb < nblk) e.rowpart[(size_t)row * nblk + gb] = -rs;
+      }
+    }
+  }
+}
+
 // the 128x128-tile kernels: 4 waves in 2x2, each 2x2 accumulators
 template <int EPI>
 __device__ __forceinline__ void epilogue(const Params& p, const Tile& t, f32x16 (&acc)[2][2],
