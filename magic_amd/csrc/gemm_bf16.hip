@@ -219,12 +219,14 @@ constexpr int WT = 256, WNT = 512;
 __device__ __attribute__((aligned(16))) int4 g_zero16[1];
 typedef __attribute__((address_space(3))) short lds_short;
 
-// operand image of one k-tile (BK = 64 or 32): NG = BK/16 DMA instructions per thread
-template <bool KC, int BK>
+// operand image of one k-tile (BK = 64 or 32) of ROWS (256 or 128) rows: NG DMA instructions
+// per thread (512 threads x 16 B each)
+template <bool KC, int BK, int ROWS = 256>
 struct WLoad {
-  static constexpr int NG = BK / 16;
+  static constexpr int NG = ROWS * BK / 4096;
   static constexpr int CPR = BK / 8;    // 16-B chunks per row of a k-contiguous image
   static constexpr int RPB = 128 / BK;  // k-contiguous rows per 256-B bank row
+  static constexpr int CPK = ROWS / 8;  // 16-B chunks per k-row of a row-contiguous image
   long long off[NG];
   int kc[NG];
   bool rv[NG];
@@ -242,8 +244,8 @@ struct WLoad {
         kc[j] = 8 * c;
         rv[j] = true;
       } else {
-        const int krow = q >> 5;
-        const int c = (q & 31) ^ (4 * (krow & 3));
+        const int krow = q / CPK;
+        const int c = (q % CPK) ^ (4 * (krow & 3));
         const int col = r0 + 8 * c;
         rv[j] = col < nrows;
         off[j] = (long long)krow * ld + col;
@@ -283,10 +285,10 @@ struct WLoad {
       const int kk = 16 * ks + 8 * (lane >> 5) + q;
       const int ro = rb + 16 * ((lane >> 4) & 1) + 4 * pp;
       const int pos = (ro >> 3) ^ (4 * (kk & 3));
-      const unsigned a0 = s_lds + 2u * (unsigned)(kk * WT + pos * 8 + (ro & 4));
+      const unsigned a0 = s_lds + 2u * (unsigned)(kk * ROWS + pos * 8 + (ro & 4));
       s16x4 lo, hi;
       asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0));
-      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a0), "i"(8 * WT));
+      asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a0), "i"(8 * ROWS));
       return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
     }
   }
@@ -538,43 +540,48 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16r_kernel(PParams pp) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Interleaved ring kernel (the default wide kernel): the operand rings, tile and epilogue of
-// gemm_bf16r_kernel, with the LDS fragment reads of the NEXT k16-step issued between the
-// MFMAs of the current one (one fragment per MFMA gap, cdna MI355X_MICROARCH.md §LDS: up to
-// three reads per 32x32x16 gap are free), so no k16-step waits for its reads and no read
-// burst stalls the MFMA issue. The iteration hand-off sits inside the last k16-step: once the
-// step's fragments are in registers every read of the iteration's images is done, so after
-// four of its MFMAs the waves wait for the next iteration's images (counted vmcnt), pass one
-// raw s_barrier, issue the copies into the slots the iteration freed, and read the next
-// iteration's first fragments behind the remaining four MFMAs.
-// Copies: B image of it+2 and A image of it+3 are issued in iteration it (B ring 2 slots,
+// Interleaved ring kernel (the default wide kernel): the operand rings of gemm_bf16r_kernel,
+// with the LDS fragment reads of the NEXT k16-step issued between the MFMAs of the current one
+// (one fragment per MFMA gap; MI355X_MICROARCH.md §LDS: up to three reads per 32x32x16 gap are
+// free), so no k16-step waits for its reads and no read burst stalls the MFMA issue. The
+// iteration hand-off sits inside the last k16-step: once the step's fragments are in registers
+// every read of the iteration's images is done, so after half of its MFMAs the waves wait for
+// the next iteration's images (counted vmcnt), pass one raw s_barrier, issue the copies into the
+// slots the iteration freed, and read the next iteration's first fragments behind the remaining
+// MFMAs. Copies: B image of it+2 and A image of it+3 are issued in iteration it (B ring 2 slots,
 // A ring 3 slots), each only when the (plane, k-tile) changes.
-template <bool AT, bool BT, int EPI, bool TE>
+// Tile 256 x TN (TN = 256 or 128), 8 waves 2 (M) x 4 (N), each 128 x TN/4 = 4 x NI 32x32
+// accumulators. TN = 128 doubles the tile count of a narrow GEMM (N ~ 500: the hidden encoder
+// and decoder layers) so it fills the chip without split-K slabs and their reduction.
+template <bool AT, bool BT, int EPI, bool TE, int TN>
 __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   constexpr int BK = 64;
-  constexpr int IMG = WT * BK;  // bf16 elements per operand image
+  constexpr int NI = TN / 128;
+  constexpr int IMA = WT * BK, IMB = TN * BK;  // bf16 elements per operand image
   constexpr int KS = BK / 16;
+  constexpr int NM = 4 * NI;                   // MFMAs per wave per k16-step
+  constexpr int NF = NI + 4;                   // fragments per wave per k16-step (B first)
   const Params& p = pp.g;
   if (epi_skip<EPI>(p.epi)) return;
-  __shared__ __attribute__((aligned(16))) short smem[5 * IMG];  // A slots 0-2 | B slots 0-1
+  __shared__ __attribute__((aligned(16))) short smem[3 * IMA + 2 * IMB];  // A slots | B slots
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
-  const Tile t = tile_of_t<WT, WT>(p, true);
+  const Tile t = tile_of_t<WT, TN>(p, true);
   const unsigned short* __restrict__ A = pp.A + t.bi * p.sA;
   const unsigned short* __restrict__ Bm = pp.B + t.bi * p.sB;
 
   WLoad<!AT, BK> la;
-  WLoad<BT, BK> lb;
+  WLoad<BT, BK, TN> lb;
   la.init(p.lda, t.m0, p.M, wave, lane);
   lb.init(p.ldb, t.n0, p.N, wave, lane);
 
-  f32x16 acc[4][2];
+  f32x16 acc[4][NI];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NI; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
@@ -585,52 +592,67 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   auto pa_of = [&](int pr) { return (pp.pab >> (4 * pr)) & 3; };
   auto pb_of = [&](int pr) { return (pp.pab >> (4 * pr + 2)) & 3; };
   auto adv = [&](int& kt, int& pr) { if (++pr == np) { pr = 0; ++kt; } };
-  // A cursor: iteration ia (k-tile, pair) of the last A image issued, its slot; B likewise
+  // A cursor: iteration ia (k-tile, pair) of the last A image considered and its slot; B likewise
   int akt = 0, apr = 0, ia = 0, asl = 0;
   int bkt = 0, bpr = 0, ib = 0, bsl = 0;
   bool pend_a = false;  // the A copy issued with the last B copy (vmcnt accounting)
-  // issue the A image of iteration ia+1 if it differs from ia's (and exists)
+  const bool dma = !(pp.diag & 1);
+  constexpr int GA = WLoad<!AT, BK>::NG;  // DMA instructions per A image per thread
+  // move the A cursor to ia+1 and copy its image if it differs from ia's
   auto next_a = [&]() -> bool {
-    if (ia + 1 >= total) return false;
+    if (ia + 1 >= total || !dma) return false;
     const int k0 = akt, p0 = apr;
     adv(akt, apr);
     ++ia;
     if (akt == k0 && pa_of(apr) == pa_of(p0)) return false;
     asl = asl == 2 ? 0 : asl + 1;
-    la.issue(A + pa_of(apr) * pp.pA, p.lda, t.ks + akt * BK, t.ke, smem + asl * IMG, wave);
+    la.issue(A + pa_of(apr) * pp.pA, p.lda, t.ks + akt * BK, t.ke, smem + asl * IMA, wave);
     return true;
   };
   auto next_b = [&]() -> bool {
-    if (ib + 1 >= total) return false;
+    if (ib + 1 >= total || !dma) return false;
     const int k0 = bkt, p0 = bpr;
     adv(bkt, bpr);
     ++ib;
     if (bkt == k0 && pb_of(bpr) == pb_of(p0)) return false;
     bsl ^= 1;
-    lb.issue(Bm + pb_of(bpr) * pp.pB, p.ldb, t.ks + bkt * BK, t.ke, smem + (3 + bsl) * IMG, wave);
+    lb.issue(Bm + pb_of(bpr) * pp.pB, p.ldb, t.ks + bkt * BK, t.ke, smem + 3 * IMA + bsl * IMB, wave);
     return true;
   };
   // slots of the images of iterations it .. it+2 (A) and it .. it+1 (B)
   int sa_q[3] = {0, 0, 0};
   int sb_q[2] = {0, 0};
 
-  bf16x8 fa[2][4], fb[2][2];
+  bf16x8 fa[2][4], fb[2][NI];
   auto rd_a = [&](int slot, int ks, int mi, bf16x8& a) {
-    a = la.frag(smem + slot * IMG, lds0 + 2u * (unsigned)(slot * IMG), wm * 128 + mi * 32, ks, lane);
+    a = la.frag(smem + slot * IMA, lds0 + 2u * (unsigned)(slot * IMA), wm * 128 + mi * 32, ks, lane);
   };
   auto rd_b = [&](int slot, int ks, int ni, bf16x8& b) {
-    b = lb.frag(smem + (3 + slot) * IMG, lds0 + 2u * (unsigned)((3 + slot) * IMG),
-                wn * 64 + ni * 32, ks, lane);
+    b = lb.frag(smem + 3 * IMA + slot * IMB, lds0 + 2u * (unsigned)(3 * IMA + slot * IMB),
+                wn * (TN / 4) + ni * 32, ks, lane);
+  };
+  // fragment f of a k16-step: B fragments first, then the four A fragments
+  auto rd_f = [&](int sa, int sb, int ks, int f, int buf) {
+    if (f < NI) rd_b(sb, ks, f, fb[buf][f]);
+    else rd_a(sa, ks, f - NI, fa[buf][f - NI]);
+  };
+  auto mfma = [&](int i, int cur) {
+    const int mi = i / NI, ni = i % NI;
+    acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][mi], fb[cur][ni], acc[mi][ni], 0, 0, 0);
   };
 
   if (total > 0) {
     // prologue: A(0), B(0), A(1); wait for A(0), B(0); barrier; B(1), A(2)
     la.issue(A + pa_of(0) * pp.pA, p.lda, t.ks, t.ke, smem, wave);
-    lb.issue(Bm + pb_of(0) * pp.pB, p.ldb, t.ks, t.ke, smem + 3 * IMG, wave);
+    lb.issue(Bm + pb_of(0) * pp.pB, p.ldb, t.ks, t.ke, smem + 3 * IMA, wave);
     const bool a1 = next_a();
     sa_q[0] = 0; sa_q[1] = asl;
-    if (a1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a1) {
+      if constexpr (GA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     next_b();
@@ -638,9 +660,7 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
     pend_a = next_a();
     sa_q[2] = asl;
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni) rd_b(sb_q[0], 0, ni, fb[0][ni]);
-#pragma unroll
-    for (int mi = 0; mi < 4; ++mi) rd_a(sa_q[0], 0, mi, fa[0][mi]);
+    for (int f = 0; f < NF; ++f) rd_f(sa_q[0], sb_q[0], 0, f, 0);
   }
   for (int it = 0; it < total; ++it) {
     const int sa = sa_q[0], sb = sb_q[0];
@@ -650,50 +670,46 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
       wait_lds<0>();  // this step's fragments (read during the previous step's MFMAs)
       __builtin_amdgcn_sched_barrier(0);
       if (ks + 1 < KS) {
-        // MFMA i, then one fragment of step ks+1 in its gap
+        // MFMA i, then the fragments of step ks+1 assigned to its gap
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int mi = i >> 1, ni = i & 1;
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][mi], fb[cur][ni], acc[mi][ni], 0, 0, 0);
+        for (int i = 0; i < NM; ++i) {
+          mfma(i, cur);
           __builtin_amdgcn_sched_barrier(0);
-          if (i < 2) rd_b(sb, ks + 1, i, fb[nx][i]);
-          else if (i < 6) rd_a(sa, ks + 1, i - 2, fa[nx][i - 2]);
+#pragma unroll
+          for (int f = 0; f < NF; ++f)
+            if (f * NM / NF == i) rd_f(sa, sb, ks + 1, f, nx);
           __builtin_amdgcn_sched_barrier(0);
         }
       } else {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int mi = i >> 1, ni = i & 1;
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][mi], fb[cur][ni], acc[mi][ni], 0, 0, 0);
-        }
+        for (int i = 0; i < NM / 2; ++i) mfma(i, cur);
         __builtin_amdgcn_sched_barrier(0);
         const bool more = it + 1 < total;
         if (more) {
           // images of it+1 landed (only the A copy issued after its B copy may be in flight),
           // every wave's reads of it's images are done: its freed slots can be refilled
-          if (pend_a) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (pend_a) {
+            if constexpr (GA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+            else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+          } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
         }
         __builtin_amdgcn_sched_barrier(0);
+        // fragments of it+1's first step (its images: the slot queues' second entries), then
+        // the copies into the freed slots: B of it+2, A of it+3
 #pragma unroll
-        for (int i = 4; i < 8; ++i) {
-          const int mi = i >> 1, ni = i & 1;
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][mi], fb[cur][ni], acc[mi][ni], 0, 0, 0);
+        for (int i = NM / 2; i < NM; ++i) {
+          mfma(i, cur);
           __builtin_amdgcn_sched_barrier(0);
           if (more) {
-            if (i == 4) {
-              // fragments of it+1's first step (its images: slot queues shifted below)
+            constexpr int H = NM / 2;  // gaps after the barrier
 #pragma unroll
-              for (int n2 = 0; n2 < 2; ++n2) rd_b(sb_q[1], 0, n2, fb[nx][n2]);
-              rd_a(sa_q[1], 0, 0, fa[nx][0]);
-            } else if (i == 5) {
-              rd_a(sa_q[1], 0, 1, fa[nx][1]);
-              rd_a(sa_q[1], 0, 2, fa[nx][2]);
-            } else if (i == 6) {
-              rd_a(sa_q[1], 0, 3, fa[nx][3]);
-              // copies into the freed slots: B of it+2, A of it+3
+            for (int f = 0; f < NF; ++f)
+              if (f * (H - 1) / NF + H == i) rd_f(sa_q[1], sb_q[1], 0, f, nx);
+            if (i == NM - 2) {
               next_b();
               sb_q[0] = sb_q[1]; sb_q[1] = bsl;
               pend_a = next_a();
@@ -708,23 +724,28 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (TE) epilogue_wide<EPI>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
-  else epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
+  if constexpr (TE) epilogue_wide<EPI, NI>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag);
+  else epilogue_g<EPI, 4, NI, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
 }
 
-template <bool AT, bool BT, int EPI, bool TE>
+template <bool AT, bool BT, int EPI, bool TE, int TN>
 hipError_t launch_q(const PParams& p, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
-  hipLaunchKernelGGL((gemm_bf16q_kernel<AT, BT, EPI, TE>), dim3(nwg), dim3(WNT), 0, st, p);
+  hipLaunchKernelGGL((gemm_bf16q_kernel<AT, BT, EPI, TE, TN>), dim3(nwg), dim3(WNT), 0, st, p);
   return hipGetLastError();
+}
+
+template <int EPI, bool TE, int TN>
+hipError_t launch_q_l(const PParams& p, bool at, bool bt, hipStream_t st) {
+  if (!at && !bt) return launch_q<false, false, EPI, TE, TN>(p, st);
+  if (at && !bt) return launch_q<true, false, EPI, TE, TN>(p, st);
+  if (!at && bt) return launch_q<false, true, EPI, TE, TN>(p, st);
+  return launch_q<true, true, EPI, TE, TN>(p, st);
 }
 
 template <int EPI, bool TE>
 hipError_t launch_q_t(const PParams& p, bool at, bool bt, hipStream_t st) {
-  if (!at && !bt) return launch_q<false, false, EPI, TE>(p, st);
-  if (at && !bt) return launch_q<true, false, EPI, TE>(p, st);
-  if (!at && bt) return launch_q<false, true, EPI, TE>(p, st);
-  return launch_q<true, true, EPI, TE>(p, st);
+  return p.g.tn == 128 ? launch_q_l<EPI, TE, 128>(p, at, bt, st) : launch_q_l<EPI, TE, 256>(p, at, bt, st);
 }
 
 template <bool AT, bool BT, int EPI, bool SP>
@@ -828,12 +849,14 @@ hipError_t launch_var(const PParams& p, bool at, bool bt, int variant, hipStream
 
 bool gemm_bf16_wide(const GemmDesc& d) {
   if (d.prec == GEMM_F32) return false;
-  if (d.variant == 1 || d.variant == 2 || d.variant == 4) return false;  // 128x128 variants
-  if (d.variant != 3 && d.variant < 5 && (d.M < 256 || d.N < 256)) return false;
+  // 10-12: default-shape variants of the interleaved kernel (old epilogue, forced tile N)
+  const int v = d.variant >= 10 ? 0 : d.variant;
+  if (v == 1 || v == 2 || v == 4) return false;  // 128x128 variants
+  if (v != 3 && v < 5 && (d.M < 256 || d.N < 256)) return false;
   // one k-tile and under a CU's worth of 256x256 tiles (dec layer 1: K = L + 1; the head's
   // dgrad: K = 2L): epilogue-bound on few CUs, the 128x128 kernels spread it wider
   const long long t256 = (long long)((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
-  if (d.variant == 0 && d.K <= 64 && t256 < 256) return false;
+  if (v == 0 && d.K <= 64 && t256 < 256) return false;
   auto a8 = [](long long v) { return (v & 7) == 0; };
   if (!a8(d.lda) || !a8(d.ldb) || !a8(d.pA) || !a8(d.pB)) return false;
   if (d.batch > 1 && (!a8(d.sA) || !a8(d.sB))) return false;
@@ -841,29 +864,49 @@ bool gemm_bf16_wide(const GemmDesc& d) {
   return true;
 }
 
-int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws) {
-  if (d.epi.mode == EPI_BCE || d.epi.mode == EPI_BCEB || d.epi.mode == EPI_SIGMOID) return 1;
-  const long long tiles = (long long)((d.M + WT - 1) / WT) * ((d.N + WT - 1) / WT) * d.batch;
+// Joint choice of the tile N (256 or 128) and split-K for the wide kernel: one 256 x TN x 64
+// k-tile per CU per iteration (one workgroup per CU) + prologue/epilogue; split-K adds the fp32
+// slab round trip and the reduction launch. Variants 11 / 12 force TN 128 / 256.
+static void wide_plan(const GemmDesc& d, size_t max_ws, int* split, int* tn) {
+  const bool fixed = d.epi.mode == EPI_BCE || d.epi.mode == EPI_BCEB || d.epi.mode == EPI_SIGMOID;
   const int kt = (d.K + 63) / 64;
   const int T = d.nA > d.nB ? d.nA : d.nB;
   int np = 0;
   for (int i = 0; i < d.nA; ++i)
     for (int j = 0; j < d.nB; ++j) np += i + j < T;
   if (d.dynA) np = (np + (d.nB < T ? d.nB : T)) / 2;  // A's residual planes often all zero
-  // one 256x256x64 k-tile per CU (one workgroup per CU); + prologue/epilogue;
-  // split-K adds the fp32 slab round trip and the reduction launch
-  const double t_kt = 1.9e-6;  // measured: 4096^3 at 1.06 PF/s = 1.94 us per k-tile per CU
   double best = 1e30;
-  int best_s = 1;
-  for (int s = 1; s <= 32; ++s) {
-    if (s > 1 && kt / s < 2) break;
-    if (s > 1 && (size_t)d.batch * s * d.M * d.N > max_ws) break;
-    const double rounds = std::ceil(tiles * s / 256.0);
-    double t = rounds * (np * std::ceil((double)kt / s) + 3.0) * t_kt;
-    if (s > 1) t += (double)d.batch * s * d.M * d.N * 8.0 / 4.5e12 + 4e-6;
-    if (t < best * 0.97) { best = t; best_s = s; }
+  *split = 1;
+  *tn = 256;
+  for (int w : {256, 128}) {
+    if (d.variant == 11 && w != 128) continue;
+    if (d.variant == 12 && w != 256) continue;
+    const long long tiles = (long long)((d.M + WT - 1) / WT) * ((d.N + w - 1) / w) * d.batch;
+    // measured: 4096^3 at 1.06 PF/s = 1.94 us per 256x256 k-tile per CU; the 256x128 tile does
+    // half the MFMA work per k-tile in ~1.5 us (profiles/r2/gemm_ab_tile_n.txt: it wins only
+    // where it removes a split-K reduction, e.g. the encoder dgrads and the 500-wide decoder)
+    const double t_kt = w == 256 ? 1.9e-6 : 1.5e-6;
+    for (int s = 1; s <= (fixed ? 1 : 32); ++s) {
+      if (s > 1 && kt / s < 2) break;
+      if (s > 1 && (size_t)d.batch * s * d.M * d.N > max_ws) break;
+      const double rounds = std::ceil(tiles * s / 256.0);
+      double t = rounds * (np * std::ceil((double)kt / s) + 3.0) * t_kt;
+      if (s > 1) t += (double)d.batch * s * d.M * d.N * 8.0 / 4.5e12 + 4e-6;
+      if (t < best * 0.97) { best = t; *split = s; *tn = w; }
+    }
   }
-  return best_s;
+}
+
+int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws) {
+  int s, tn;
+  wide_plan(d, max_ws, &s, &tn);
+  return s;
+}
+
+int gemm_bf16_wide_tn(const GemmDesc& d, size_t max_ws) {
+  int s, tn;
+  wide_plan(d, max_ws, &s, &tn);
+  return tn;
 }
 
 hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, hipStream_t st) {
@@ -885,8 +928,12 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   p.pab = 0;
   for (int i = 0; i < n; ++i) p.pab |= (p.pa[i] | p.pb[i] << 2) << (4 * i);
   if (gemm_bf16_wide(d)) {
+    // tile N: the planner's (gemm_run), 256 for the diagnostic variants of the 256x256 forms
+    const bool q = d.variant == 0 || d.variant == 3 || d.variant == 10 || d.variant == 11 ||
+                   d.variant == 12;
+    p.g.tn = q && g.tn == 128 ? 128 : 256;
     p.g.ntm = (d.M + WT - 1) / WT;
-    p.g.ntn = (d.N + WT - 1) / WT;
+    p.g.ntn = (d.N + p.g.tn - 1) / p.g.tn;
     switch (epi) {
       case EPI_STORE: return launch_wide<EPI_STORE>(p, d.at, d.bt, d.variant, st);
       case EPI_ACT: return launch_wide<EPI_ACT>(p, d.at, d.bt, d.variant, st);

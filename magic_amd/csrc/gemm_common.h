@@ -20,6 +20,7 @@ struct Params {
   long long sA, sB, sC;     // batch strides
   int batch, split, kchunk;
   int ntm, ntn;
+  int tn;                   // wide bf16 kernel: tile N (256 or 128)
   GemmEpi epi;
 };
 
@@ -239,35 +240,40 @@ __device__ __forceinline__ void st8_planes(unsigned short* cp, long long pc, int
   }
 }
 
-template <int EPI>
-__device__ __forceinline__ void epilogue_wide(const Params& p, const Tile& t, f32x16 (&acc)[4][2],
-                                              float* lds, int wm, int wn) {
-  constexpr int TW = 256, BAND = 64 * TW;  // floats per band buffer
+// diag (timing diagnostics, results meaningless): bit 1 = no global stores, bit 2 = no LDS
+// transpose, bit 3 = no transcendental math. Tile 256 x 128*NI (waves 2 x 4, acc [4][NI]).
+template <int EPI, int NI>
+__device__ __forceinline__ void epilogue_wide(const Params& p, const Tile& t, f32x16 (&acc)[4][NI],
+                                              float* lds, int wm, int wn, int diag = 0) {
+  constexpr int TW = 128 * NI, BAND = 64 * TW;  // band row width, floats per band buffer
+  constexpr int CW = TW / 8;                    // 8-column chunks per band row
+  constexpr int RP = 512 / CW;                  // band rows per reader pass
   constexpr bool BCE = EPI == EPI_BCE || EPI == EPI_BCEB;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const GemmEpi& e = p.epi;
   float* __restrict__ C = p.C + (size_t)t.z * p.sC;
   unsigned short* __restrict__ cp = e.cp ? e.cp + (size_t)t.z * p.sC : nullptr;
-  const int c8 = tid & 31, rr = tid >> 5;   // reader: chunk of 8 columns, row within 16
+  const int c8 = tid % CW, rr = tid / CW;   // reader: chunk of 8 columns, row within RP
   const int col0 = t.n0 + 8 * c8;
   const int nblk = (p.N + 127) / 128;
-  const int gb = t.nt * 2 + (c8 >> 4);      // 128-column block of this chunk
+  const int gb = t.nt * NI + (c8 >> 4);     // 128-column block of this chunk
 #pragma unroll
   for (int mi = 0; mi < 4; ++mi) {
     float* band = lds + (mi & 1) * BAND;
-    // writer: this wave's 32 x 64 block of the band, C/D layout -> row-major
+    // writer: this wave's 32 x (TW/4) block of the band, C/D layout -> row-major
+    if (!(diag & 4))
 #pragma unroll
-    for (int ni = 0; ni < 2; ++ni)
+    for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        band[row * TW + wn * 64 + ni * 32 + (lane & 31)] = acc[mi][ni][r];
+        band[row * TW + wn * (TW / 4) + ni * 32 + (lane & 31)] = acc[mi][ni][r];
       }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int br = rr + 16 * q;                               // band row
+    for (int q = 0; q < 64 / RP; ++q) {
+      const int br = rr + RP * q;                                    // band row
       const int row = t.m0 + (br >> 5) * 128 + mi * 32 + (br & 31);  // tile row -> global
       float v[8];
       const float4 a = *reinterpret_cast<const float4*>(band + br * TW + 8 * c8);
@@ -313,6 +319,7 @@ __device__ __forceinline__ void epilogue_wide(const Params& p, const Tile& t, f3
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
           if constexpr (BCE) {
+            if (diag & 8) { yv[j] = v[j]; rs += v[j] * sv[j]; v[j] = (yv[j] - sv[j]) * e.scale; continue; }
             yv[j] = sigmoid_fast(v[j]);
             // -log(y^x (1-y)^(1-x)) with TF pow(0,0) = 1 (no epsilon), 11a/vae.py:266-269
             if (j < nv) rs += bce_term(yv[j], sv[j]);
@@ -323,7 +330,8 @@ __device__ __forceinline__ void epilogue_wide(const Params& p, const Tile& t, f3
           if constexpr (EPI == EPI_DACT) v[j] = dact_f(v[j], sv[j], e.act);
         }
         const size_t o = (size_t)row * p.ldc + col0;
-        if (full) {
+        if (diag & 2) {
+        } else if (full) {
           if (e.c32) st8f(C + o, v);
           if (cp) st8_planes(cp, e.pc, e.ncp, o, v);
           if constexpr (BCE)

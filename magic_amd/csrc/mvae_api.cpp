@@ -1051,11 +1051,42 @@ extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int
     d.Ap = A_.p; d.pA = A_.stride; d.nA = np;
     d.Bp = B_.p; d.pB = B_.stride; d.nB = np;
   }
+  // epi bit 12 (plane modes): the output as bf16 planes only (no fp32 store), as the step's
+  // producers write their operand images; C then receives the planes' sum (host side)
+  const bool planes_out = ((epi >> 12) & 1) && d.prec != GEMM_F32;
+  const int npc = d.prec == GEMM_BF16 ? 1 : 3;
+  const size_t nc = (size_t)M * ldc;
+  unsigned short* cpl = nullptr;
+  if (e == hipSuccess && planes_out) {
+    e = hipMalloc(&cpl, npc * nc * 2);
+    if (e == hipSuccess) e = hipMemsetAsync(cpl, 0, npc * nc * 2, st);
+    d.epi.cp = cpl; d.epi.pc = (long long)nc; d.epi.ncp = npc; d.epi.c32 = 0;
+  }
   const size_t ws_n = gemm_workspace_elems(d);
   float* ws = nullptr;
   if (e == hipSuccess && ws_n) e = hipMalloc(&ws, ws_n * sizeof(float));
   if (e == hipSuccess) e = gemm_run(d, ws, ws_n, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e == hipSuccess && planes_out) {
+    std::vector<unsigned short> h(npc * nc);
+    std::vector<float> c(nc);
+    e = hipMemcpy(h.data(), cpl, h.size() * 2, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(c.data(), Cm, nc * 4, hipMemcpyDeviceToHost);
+    for (int r = 0; e == hipSuccess && r < M; ++r)
+      for (int j = 0; j < N; ++j) {
+        const size_t o = (size_t)r * ldc + j;
+        float v = 0.f;
+        for (int t = npc - 1; t >= 0; --t) {
+          uint32_t u = (uint32_t)h[t * nc + o] << 16;
+          float f;
+          std::memcpy(&f, &u, 4);
+          v += f;
+        }
+        c[o] = v;
+      }
+    if (e == hipSuccess) e = hipMemcpy(Cm, c.data(), nc * 4, hipMemcpyHostToDevice);
+  }
+  if (cpl) (void)hipFree(cpl);
   if (ws) (void)hipFree(ws);
   for (void* q : tmp) if (q) (void)hipFree(q);
   if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }

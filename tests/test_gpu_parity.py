@@ -68,11 +68,14 @@ def _padded(rows, cols, g):
 @pytest.mark.parametrize("M,N,K,variant", [(256, 256, 64, 3), (300, 517, 1001, 3), (1000, 600, 4099, 0),
                                            (513, 260, 130, 0), (40, 70, 200, 3), (1000, 600, 4099, 8),
                                            (300, 517, 1001, 7), (513, 260, 130, 7), (40, 70, 200, 7),
-                                           (256, 256, 64, 7)])
+                                           (256, 256, 64, 7), (300, 517, 1001, 6), (1000, 600, 4099, 11),
+                                           (513, 260, 130, 11), (300, 517, 1001, 11), (1000, 600, 4099, 12),
+                                           (2100, 500, 700, 11)])
 def test_gemm_wide_kernel(at, bt, M, N, K, variant, prec):
-    """The 256x256 LDS-DMA bf16 kernel (variant 3 forces it; 0 lets the planner pick it for
-    M, N >= 256: the operand-ring form; 7 adds s_setprio, 8 is the two-stage form) on every layout,
-    ragged edges and split-K, against float64."""
+    """The 256-row LDS-DMA bf16 kernels (variant 3 forces the interleaved ring kernel; 0 lets the
+    planner pick it and its tile N for M, N >= 256; 11 / 12 force tile N 128 / 256; 6 is the round-1
+    ring form, 7 the same with s_setprio, 8 the two-stage form) on every layout, ragged edges and
+    split-K, against float64."""
     lib = _lib.load()
     g = torch.Generator(device="cuda").manual_seed(M * 5 + N * 11 + K)
     A = _padded(K, M, g) if at else _padded(M, K, g)
@@ -439,10 +442,14 @@ def test_step_bf16_documented_tolerance():
 # ------------------------------------------------------------------ 256x256 kernel paths
 @pytest.mark.parametrize("prec", [2, 1], ids=["f32x", "bf16"])
 @pytest.mark.parametrize("epi,act", [(1, 0), (1, 1), (2, 0), (2, 1), (4, 0)])
-@pytest.mark.parametrize("M,N,ldc", [(600, 520, 520), (300, 500, 500), (513, 257, 260), (280, 300, 301)])
-def test_gemm_wide_epilogues(prec, epi, act, M, N, ldc):
-    """Fused epilogues of the 256x256 kernel (LDS-transposed 16-B row stores; scalar tails on
-    ragged columns and unaligned rows) against float64; nothing written past column N."""
+@pytest.mark.parametrize("M,N,ldc", [(600, 520, 520), (300, 500, 500), (513, 257, 264), (280, 300, 301)])
+@pytest.mark.parametrize("variant,planes", [(0, 0), (0, 1), (11, 1), (12, 1), (11, 0)])
+def test_gemm_wide_epilogues(prec, epi, act, M, N, ldc, variant, planes):
+    """Fused epilogues of the wide kernels against float64; nothing written past column N.
+    planes=1 writes the output as bf16 planes only (as the step's producers do), which takes the
+    LDS-staged row-major epilogue (16-B chunk stores, element stores on ragged tails; ld 301 is
+    not 16-B aligned and falls back to the C/D-layout epilogue); fp32-only outputs keep the C/D
+    layout. Variants 11 / 12 force tile N 128 / 256."""
     lib = _lib.load()
     K = 304
     g = torch.Generator(device="cuda").manual_seed(M + 7 * N + 31 * epi + act)
@@ -453,7 +460,8 @@ def test_gemm_wide_epilogues(prec, epi, act, M, N, ldc):
     aux = torch.tanh(pre) if act == 0 else torch.nn.functional.elu(pre)
     C = torch.full((M, ldc), float("nan"), device="cuda")
     rc = lib.mvae_debug_gemm(M, N, K, A.data_ptr(), K, 0, Bm.data_ptr(), Bm.shape[1], 0, C.data_ptr(),
-                             ldc, epi | (prec << 4), act, aux.data_ptr(), ld_aux,
+                             ldc, epi | (prec << 4) | (variant << 8) | (planes << 12), act,
+                             aux.data_ptr(), ld_aux,
                              torch.cuda.current_stream().cuda_stream)
     assert rc == 0, lib.mvae_last_error(None)
     acc = A.double() @ Bm[:, :N].double()
@@ -466,9 +474,11 @@ def test_gemm_wide_epilogues(prec, epi, act, M, N, ldc):
         ref = torch.sigmoid(acc)
     mag = (A.double().abs() @ Bm[:, :N].double().abs()).max().item()
     bound = (2e-6 if prec == 2 else 1e-2) * mag + 1e-6
+    if planes and prec == 1:  # one RN bf16 plane of the output
+        bound += 2.0 ** -8 * ref.abs().max().item()
     err = (C[:, :N].double() - ref).abs().max().item()
     assert err <= bound, (err, bound)
-    if ldc > N:
+    if ldc > N and not planes:
         assert torch.isnan(C[:, N:]).all()
 
 
