@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MVAE_ABI_VERSION 2
+#define MVAE_ABI_VERSION 3
 #define MVAE_MAX_ENC 8
 
 enum { MVAE_OK = 0, MVAE_EINVAL = -1, MVAE_ECONFIG = -2, MVAE_ESTATE = -3 };
@@ -65,6 +65,14 @@ typedef struct mvae_cfg {
   float beta1, beta2, epsilon; /* TF AdamOptimizer defaults .9/.999/1e-8       */
   int precision;         /* MVAE_PREC_*                                         */
   uint64_t seed;         /* counter-based N(0,1) stream for eps when not given */
+  int conv;              /* 1: conv-encoder variant (BASELINE config 5): the CifarNet
+                            tower of 6b/net.py:50-60 (conv5x5x64, pool, LRN, conv5x5x64,
+                            LRN, pool; weights shared by the three encoder passes) in front
+                            of the FC encoder, whose first layer then reads the (S/4)^2*64
+                            tower features. Variables enc_conv{1,2}_{W,b} come first in
+                            mvae_param_info order (W as [25*c_in, 64], TF HWIO flattened).
+                            Needs image_size % 4 == 0. bf16 precision runs the 64->64 conv
+                            on MFMA; f32 / f32x run the tower in fp32. 0: FC encoder.  */
 } mvae_cfg;
 
 typedef struct mvae_ctx mvae_ctx;
@@ -193,6 +201,13 @@ int mvae_timing_reset(mvae_ctx* ctx);
  * (synchronous; tests only). mvae_bench_gemm: variant | (prec << 4) | (epi << 8).    */
 int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, int variant, int iters,
                     void* stream, float* avg_ms);
+/* One 5x5x64x64 conv kernel of the conv tower on caller data (tests; synchronous): S1 x S1 x 64
+ * NHWC images, B rows (3B forward images, 4B backward). mode 0: relu(conv(x, W2) + b2), 3B
+ * images, y = W2 block [1601][64]; mode 1: data gradient of x (4B images), y = W2; mode 2:
+ * out[2][1601][64] = the cost / metric weight gradients of x = conv2 input (3B), y = d pre-
+ * activation (4B). mfma: bf16 MFMA kernels (operands rounded to bf16), else fp32 VALU.     */
+int mvae_debug_conv2(int S1, int B, int mode, int mfma, const float* x, const float* y, float* out,
+                     void* stream);
 int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int at, const float* B, int ldb,
                     int bt, float* C, int ldc, int epi, int act, const float* aux, int ld_aux,
                     void* stream);

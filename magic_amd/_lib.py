@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("MVAE_LIB", os.path.join(HERE, "libmvae.so"))
 
 MVAE_MAX_ENC = 8
 MARKER_GRID = 4096   # mvae_region_marker workgroups = MARKER_GRID + region (mvae_internal.h)
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 ACT = {"tanh": 0, "elu": 1}
 METRIC = {"cosine": 0, "sqdiff": 1}
@@ -42,7 +42,7 @@ class mvae_cfg(C.Structure):
         ("latent", C.c_int), ("act", C.c_int), ("metric", C.c_int), ("reciprocal", C.c_int),
         ("deform_weight", C.c_float), ("lr", C.c_float * 2),
         ("beta1", C.c_float), ("beta2", C.c_float), ("epsilon", C.c_float),
-        ("precision", C.c_int), ("seed", C.c_uint64),
+        ("precision", C.c_int), ("seed", C.c_uint64), ("conv", C.c_int),
     ]
 
 
@@ -89,6 +89,8 @@ _SIGS = {
     "mvae_timing_reset": ([C.c_void_p], C.c_int),
     "mvae_bench_gemm": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                          C.c_void_p, C.POINTER(C.c_float)], C.c_int),
+    "mvae_debug_conv2": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                          C.c_void_p], C.c_int),
     "mvae_debug_gemm": ([C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p,
                          C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                          C.c_int, C.c_void_p], C.c_int),

@@ -29,6 +29,7 @@ class MVAEConfig:
     epsilon: float = 1e-8
     precision: str = "f32"
     seed: int = 2
+    conv: bool = False   # conv-encoder variant: CifarNet tower (6b/net.py:50-60) before the FC encoder
 
     @property
     def D(self) -> int:
@@ -45,14 +46,22 @@ class MVAEConfig:
         """Algorithmic FLOPs of one training pair: 3 encoder forwards,
         1 decoder forward, decoder backward, 4 encoder backward passes (lock x2, rot, key)."""
         D, L = self.D, self.latent
-        widths = [D] + list(self.enc)
+        S1 = self.image_size // 2
+        F0 = (S1 // 2) ** 2 * 64 if self.conv else D      # layer-0 fan-in
+        widths = [F0] + list(self.enc)
         enc_fwd = sum(2 * a * b for a, b in zip(widths[:-1], widths[1:])) + 2 * self.enc[-1] * 2 * L
         dec_layers = [(L, self.dec[0]), (self.dec[0], self.dec[1]), (self.dec[1], D)]
         dec_fwd = sum(2 * a * b for a, b in dec_layers)
         dec_bwd = 2 * dec_fwd  # wgrad + dgrad (the dgrad into z is counted, cheap)
         # encoder backward per pass: wgrad of every layer + dgrad of every layer but the first
+        # (the first is conv1 in the conv variant: 25 MACs x 64 per pixel; conv2: 1600 x 64
+        # per pooled pixel)
+        first = 2 * F0 * self.enc[0]
+        if self.conv:
+            first = 2 * D * 25 * 64
+            enc_fwd += first + 2 * S1 * S1 * 1600 * 64
         enc_w = enc_fwd
-        enc_d = enc_fwd - 2 * D * self.enc[0]
+        enc_d = enc_fwd - first
         enc_bwd = 4 * (enc_w + enc_d)
         return float(3 * enc_fwd + dec_fwd + dec_bwd + enc_bwd)
 
@@ -100,4 +109,8 @@ def baseline_config(cid: str) -> MVAEConfig:
         return preset("8d", batch=8192, precision="bf16")
     if cid == "C5":
         return preset("8e", batch=8192, metric="sqdiff", reciprocal=True, precision="bf16")
+    if cid == "C5CONV":
+        # BASELINE config 5's conv-encoder variant: the CifarNet tower in front of the 8e
+        # encoder (latent 2000, reciprocal squared difference), bf16 MFMA
+        return preset("8e", batch=512, metric="sqdiff", reciprocal=True, precision="bf16", conv=True)
     raise KeyError(cid)

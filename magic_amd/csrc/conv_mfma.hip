@@ -1,0 +1,295 @@
+// bf16-MFMA kernels of the conv tower's 5x5x64x64 layer (conv_tower.hip; bf16 mode), gfx950
+// v_mfma_f32_32x32x16_bf16 with fp32 accumulate.
+//
+// conv2_mfma_kernel — the SAME convolution as an implicit GEMM (forward, and the data gradient
+// with the rotated/transposed kernel image): M = output pixels of a band of BR image rows,
+// N = 64 output channels, K = 25 taps x 64 input channels. The band's input patch
+// ((BR+4) x (S1+4) pixels x 64 channels, zero border) sits in LDS once; each tap's 64x64 kernel
+// slice streams through a double-buffered LDS slot (one barrier per tap). A tap is a constant
+// shift of every lane's patch address, so the A fragments are plain 16-B ds_read_b128 of the
+// shifted pixel rows; 16-B chunks are XOR-swizzled by (pixel>>1)&7 so 16 consecutive pixels hit
+// 16 distinct bank slots. 4 waves x (2 M-fragments of 32 pixels) x (2 N-fragments): 256 pixel
+// slots; for S1 = 50 a band is 5 rows = 250 pixels. LDS 78.6 KB: two workgroups per CU, so one
+// stages its patch while the other computes.
+//
+// conv2_wgrad_mfma_kernel — dW[t][k][n] = sum_p in[p + t][k] d[p][n]: K = pixels, so both
+// operands are pixel-major ([pixel][channel] rows) and are read with ds_read_b64_tr_b16 (each
+// lane of a 16-lane group addresses its own pixel row: the tap shift is again a constant
+// offset). A workgroup owns one 32-channel half of k and of n for all 25 taps (accumulators
+// spread over 4 waves by tap), over a chunk of images; the four (k, n) halves of one chunk are
+// placed on the same XCD so their shared operand rows hit that XCD's L2.
+#include "mvae_internal.h"
+#include <algorithm>
+
+namespace mvae {
+namespace {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef short s16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+constexpr int CH = 64, NT = 25;
+
+__device__ __forceinline__ int swz(int px) { return (px >> 1) & 7; }
+
+template <bool FWD>
+__global__ __launch_bounds__(256, 2) void conv2_mfma_kernel(const unsigned short* __restrict__ in,
+                                                            const unsigned short* __restrict__ wimg,
+                                                            const float* __restrict__ bias,
+                                                            float* __restrict__ out, int S1, int BR) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  const int PW = S1 + 4, PR = BR + 4;
+  unsigned short* patch = lds;                 // [PR*PW][64], 16-B chunks swizzled
+  unsigned short* wb = lds + PR * PW * CH;     // 2 x [64 n][64 k], swizzled by n
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int img = blockIdx.y;
+  const int y0 = blockIdx.x * BR;
+  const int rows = min(BR, S1 - y0);
+  const int npx = rows * S1;
+  const size_t ibase = (size_t)img * S1 * S1 * CH;
+  // a tap's 64x64 slice = 512 16-B chunks, two per thread: chunk q -> n = q/8, k chunk q%8
+  int4 wr0 = *reinterpret_cast<const int4*>(wimg + 8 * tid);
+  int4 wr1 = *reinterpret_cast<const int4*>(wimg + 8 * (tid + 256));
+  for (int i = tid; i < PR * PW * 8; i += 256) {
+    const int px = i >> 3, c = i & 7;
+    const int y = y0 - 2 + px / PW, x = px % PW - 2;
+    int4 v = make_int4(0, 0, 0, 0);
+    if (y >= 0 && y < S1 && x >= 0 && x < S1)
+      v = *reinterpret_cast<const int4*>(in + ibase + ((size_t)y * S1 + x) * CH + 8 * c);
+    *reinterpret_cast<int4*>(patch + px * CH + 8 * (c ^ swz(px))) = v;
+  }
+  auto put_w = [&](unsigned short* dst) {
+    const int n0 = tid >> 3, n1 = n0 + 32, c = tid & 7;
+    *reinterpret_cast<int4*>(dst + n0 * CH + 8 * (c ^ swz(n0))) = wr0;
+    *reinterpret_cast<int4*>(dst + n1 * CH + 8 * (c ^ swz(n1))) = wr1;
+  };
+  put_w(wb);
+  __syncthreads();
+  const int nfr = (npx + 31) >> 5;
+  const bool has0 = wave < nfr, has1 = wave + 4 < nfr;  // wave-uniform
+  int pb[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int pl = (wave + 4 * i) * 32 + (lane & 31);
+    const int q = pl < npx ? pl : 0;
+    pb[i] = (q / S1) * PW + q % S1;
+  }
+  const int h = lane >> 5;
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  for (int t = 0; t < NT; ++t) {
+    const unsigned short* wc = wb + (t & 1) * CH * CH;
+    if (t + 1 < NT) {
+      wr0 = *reinterpret_cast<const int4*>(wimg + (size_t)(t + 1) * CH * CH + 8 * tid);
+      wr1 = *reinterpret_cast<const int4*>(wimg + (size_t)(t + 1) * CH * CH + 8 * (tid + 256));
+    }
+    const int toff = (t / 5) * PW + t % 5;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int c = 2 * ks + h;
+      bf16x8 fa[2], fb[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int px = pb[i] + toff;
+        fa[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(patch + px * CH + 8 * (c ^ swz(px))));
+      }
+#pragma unroll
+      for (int nf = 0; nf < 2; ++nf) {
+        const int n = nf * 32 + (lane & 31);
+        fb[nf] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(wc + n * CH + 8 * (c ^ swz(n))));
+      }
+      if (has0) {
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[0][1], 0, 0, 0);
+      }
+      if (has1) {
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[1][1], 0, 0, 0);
+      }
+    }
+    if (t + 1 < NT) put_w(wb + ((t + 1) & 1) * CH * CH);
+    __syncthreads();
+  }
+  // C: row (pixel) (r&3) + 8(r>>2) + 4h of the fragment, column (channel) lane&31 + 32 nf
+  const size_t obase = ibase + (size_t)y0 * S1 * CH;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    if (!(i ? has1 : has0)) continue;
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) {
+      const int n = nf * 32 + (lane & 31);
+      const float b = FWD ? bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int pl = (wave + 4 * i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (pl >= npx) continue;
+        float v = acc[i][nf][r];
+        if (FWD) v = fmaxf(v + b, 0.f);
+        out[obase + (size_t)pl * CH + n] = v;
+      }
+    }
+  }
+}
+
+// Weight gradient. Grid: 8 * ceil(2 * nchunk * 4 / 8) workgroups; id -> (XCD = id & 7,
+// sibling s = (id >> 3) & 3 = k half * 2 + n half, chunk group). LDS: the image rows of one row
+// block [r0, r0 + R) for one channel half: A patch (R+4) x (S1+4) x 32 and d 16*nk x 32 (64-B
+// pixel rows: four consecutive pixels of a tr16 group span the 256-B bank row, no swizzle).
+__global__ __launch_bounds__(256, 2) void conv2_wgrad_mfma_kernel(const unsigned short* __restrict__ inb,
+                                                                  const unsigned short* __restrict__ db,
+                                                                  int S1, int R, int B2, int nchunk, int ipc,
+                                                                  float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  const int PW = S1 + 4;
+  const int nslot = ((R * S1 + 15) / 16) * 16;   // pixel slots of a row block (k16 steps * 16)
+  unsigned short* ap = lds;                      // [(R+4)*PW][32]
+  unsigned short* dp = lds + (R + 4) * PW * 32;  // [nslot][32]
+  const int id = blockIdx.x;
+  const int xcd = id & 7, sib = (id >> 3) & 3, cgi = (id >> 5) * 8 + xcd;
+  if (cgi >= 2 * nchunk) return;                 // workgroup-uniform
+  const int grp = cgi / nchunk, chunk = cgi % nchunk;
+  const int kh = sib >> 1, nh = sib & 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j0 = grp * B2 + chunk * ipc;
+  const int j1 = min(j0 + ipc, grp * B2 + B2);
+  const int np1 = S1 * S1;
+  // taps of this wave: wave, wave + 4, ... (7, 6, 6, 6); bias (ones A fragment) on wave 3 of kh 0
+  constexpr int MT = 7;
+  f32x16 acc[MT], accb;
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) accb[r] = 0.f;
+  const bool dobias = kh == 0 && wave == 3;
+  const int i16 = lane & 15, q = i16 >> 2, pq = i16 & 3, h = lane >> 5, g1 = (lane >> 4) & 1;
+  const int col = 16 * g1 + 4 * pq;             // this lane's 4-element column chunk
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  for (int j = j0; j < j1; ++j) {
+    const int f = j < B2 ? j : j - B2 / 2;
+    for (int r0 = 0; r0 < S1; r0 += R) {
+      const int rows = min(R, S1 - r0);
+      const int npx = rows * S1;
+      __syncthreads();
+      for (int i = tid; i < (R + 4) * PW * 4; i += 256) {   // 16-B chunks, 4 per 32-channel row
+        const int px = i >> 2, c = i & 3;
+        const int y = r0 - 2 + px / PW, x = px % PW - 2;
+        int4 v = make_int4(0, 0, 0, 0);
+        if (y >= 0 && y < S1 && x >= 0 && x < S1)
+          v = *reinterpret_cast<const int4*>(inb + ((size_t)f * np1 + y * S1 + x) * CH + 32 * kh + 8 * c);
+        *reinterpret_cast<int4*>(ap + px * 32 + 8 * c) = v;
+      }
+      for (int i = tid; i < nslot * 4; i += 256) {
+        const int p = i >> 2, c = i & 3;
+        int4 v = make_int4(0, 0, 0, 0);
+        if (p < npx) v = *reinterpret_cast<const int4*>(db + ((size_t)j * np1 + (size_t)r0 * S1 + p) * CH + 32 * nh + 8 * c);
+        *reinterpret_cast<int4*>(dp + p * 32 + 8 * c) = v;
+      }
+      __syncthreads();
+      for (int s = 0; s < nslot / 16; ++s) {
+        const int klo = 16 * s + 8 * h + q, khi = klo + 4;
+        const int plo = klo < npx ? klo : 0, phi = khi < npx ? khi : 0;
+        const int alo = (plo / S1) * PW + plo % S1, ahi = (phi / S1) * PW + phi % S1;
+        const s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(dp + klo * 32 + col));
+        const s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(dp + khi * 32 + col));
+        const bf16x8 fb = __builtin_bit_cast(bf16x8, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int i = 0; i < MT; ++i) {
+          const int t = wave + 4 * i;
+          if (t >= NT) break;
+          const int toff = (t / 5) * PW + t % 5;
+          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ap + (alo + toff) * 32 + col));
+          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ap + (ahi + toff) * 32 + col));
+          const bf16x8 fa = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[i], 0, 0, 0);
+        }
+        if (dobias) accb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb, accb, 0, 0, 0);
+      }
+    }
+  }
+  float* out = slab + ((size_t)grp * nchunk + chunk) * (NT * CH + 1) * CH;
+  const int n = 32 * nh + (lane & 31);
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int t = wave + 4 * i;
+    if (t >= NT) break;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * h;
+      out[(size_t)(t * CH + k) * CH + n] = acc[i][r];
+    }
+  }
+  if (dobias && h == 0) out[(size_t)NT * CH * CH + n] = accb[0];
+}
+
+// bf16 kernel images of conv2 for the MFMA kernels, [t][n][k] (k contiguous):
+// forward  wf[t][n][k] = W[t*64 + k][n];  data gradient  wd[t][n][k] = W[(24 - t)*64 + n][k]
+__global__ void conv2_wprep_kernel(const float* __restrict__ W, unsigned short* __restrict__ wf,
+                                   unsigned short* __restrict__ wd) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= NT * CH * CH) return;
+  const int t = i / (CH * CH), n = (i / CH) % CH, k = i % CH;
+  wf[i] = __builtin_bit_cast(unsigned short, __float2bfloat16(W[(size_t)(t * CH + k) * CH + n]));
+  wd[i] = __builtin_bit_cast(unsigned short, __float2bfloat16(W[(size_t)((NT - 1 - t) * CH + n) * CH + k]));
+}
+
+}  // namespace
+
+int conv2_mfma_band(int S1) {
+  int br = std::max(1, std::min(S1, 256 / S1));
+  while (br > 1 && (size_t)(br + 4) * (S1 + 4) * CH * 2 + 2 * CH * CH * 2 > 160 * 1024) --br;
+  return br;
+}
+
+size_t conv2_mfma_lds(int S1) {
+  const int br = conv2_mfma_band(S1);
+  return (size_t)(br + 4) * (S1 + 4) * CH * 2 + 2 * CH * CH * 2;
+}
+
+int conv2_wgrad_rows(int S1) { return std::max(1, std::min(S1, 256 / S1)); }
+
+size_t conv2_wgrad_lds(int S1) {
+  const int R = conv2_wgrad_rows(S1);
+  const size_t nslot = ((size_t)R * S1 + 15) / 16 * 16;
+  return ((size_t)(R + 4) * (S1 + 4) + nslot) * 32 * 2;
+}
+
+hipError_t launch_conv2_wprep(const ConvTower& T, const float* w2, hipStream_t st) {
+  hipLaunchKernelGGL(conv2_wprep_kernel, dim3((NT * CH * CH + 255) / 256), dim3(256), 0, st, w2, T.w2f, T.w2d);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv2_mfma(const ConvTower& T, bool fwd, const unsigned short* inb,
+                             const unsigned short* wimg, const float* w2, float* out, int nimg,
+                             hipStream_t st) {
+  const int br = conv2_mfma_band(T.S1);
+  const size_t lds = conv2_mfma_lds(T.S1);
+  dim3 g((T.S1 + br - 1) / br, nimg);
+  const float* bias = w2 + (size_t)NT * CH * CH;
+  if (fwd)
+    hipLaunchKernelGGL(conv2_mfma_kernel<true>, g, dim3(256), lds, st, inb, wimg, bias, out, T.S1, br);
+  else
+    hipLaunchKernelGGL(conv2_mfma_kernel<false>, g, dim3(256), lds, st, inb, wimg, bias, out, T.S1, br);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv2_wgrad_mfma(const ConvTower& T, int B, hipStream_t st) {
+  const int B2 = 2 * B;
+  const int nchunk = T.nchunk2m, ipc = (B2 + nchunk - 1) / nchunk;
+  const int groups8 = (2 * nchunk + 7) / 8;
+  hipLaunchKernelGGL(conv2_wgrad_mfma_kernel, dim3(groups8 * 32), dim3(256), conv2_wgrad_lds(T.S1), st,
+                     T.n1b, T.da2b, T.S1, conv2_wgrad_rows(T.S1), B2, nchunk, ipc, T.slab);
+  return hipGetLastError();
+}
+
+}  // namespace mvae

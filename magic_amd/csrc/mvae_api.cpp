@@ -47,6 +47,16 @@ struct mvae_ctx {
   // parameters
   std::vector<Block> enc;
   Block head, v1, v2, vo;
+  // conv-encoder variant (cfg.conv): tower blocks [25*c_in; b] x 64 before the FC encoder
+  bool conv = false;
+  Block cv1, cv2;
+  ConvTower tower;
+  int F = 0, ldf = 0;        // tower features per image (FC layer-0 fan-in) and row stride
+  float* xf = nullptr;       // [3B][ldf] tower features (+ ones column): FC layer-0 operand
+  float* dxf = nullptr;      // [4B][ldf] their gradient
+  int xf32 = 1;              // write the fp32 xf rows (some fp32 GEMM reads them)
+  GemmDesc bwd_feat;         // dxf = dZ_0 W_0^T
+  int bwd_feat_r = 0;
   size_t n_all = 0, n_enc = 0;
   float* theta = nullptr;
   float* grads = nullptr;
@@ -207,9 +217,11 @@ static void build_schedule(mvae_ctx* c) {
   const long long n_all = (long long)c->n_all;
   // ---- forward: encoder on the stacked 3B rows
   c->fwd_enc.clear();
+  const float* X0 = c->conv ? c->xf : c->xs;   // layer-0 operand: pixels or tower features
+  const int ld0 = c->conv ? c->ldf : c->ldx;
   for (int i = 0; i < n; ++i) {
-    const float* A = i == 0 ? c->xs : c->H[i - 1];
-    const int lda = i == 0 ? c->ldx : c->ldh[i - 1];
+    const float* A = i == 0 ? X0 : c->H[i - 1];
+    const int lda = i == 0 ? ld0 : c->ldh[i - 1];
     GemmDesc d = gd(3 * B, c->enc[i].N, c->enc[i].K + 1, A, lda, false, th + c->enc[i].off,
                     c->enc[i].ld, false, c->H[i], c->ldh[i], EPI_ACT);
     d.epi.act = act;
@@ -278,8 +290,8 @@ static void build_schedule(mvae_ctx* c) {
   auto wgrad = [&](int i) {  // [W_i; b_i] gradients (g1 and g2 as one batch-2 GEMM); i == n: head
     const bool head = i == n;
     const Block& blk = head ? c->head : c->enc[i];
-    const float* A = i == 0 ? c->xs : c->H[i - 1];
-    const int lda = i == 0 ? c->ldx : c->ldh[i - 1];
+    const float* A = i == 0 ? X0 : c->H[i - 1];
+    const int lda = i == 0 ? ld0 : c->ldh[i - 1];
     const float* src = head ? c->dhead : c->dzl[i];
     const int lds = head ? c->ld_dh : c->lddz;
     GemmDesc w = gd(blk.K + 1, blk.N, 2 * B, A, lda, true, src, lds, false, g1 + blk.off, blk.ld);
@@ -288,6 +300,11 @@ static void build_schedule(mvae_ctx* c) {
     c->bwd_enc_r.push_back(region(c, head ? std::string("head_bwd_w") : "enc_bwd_w_" + std::to_string(i)));
   };
   for (int i = n; i >= 1; --i) dgrad(i);
+  if (c->conv) {  // gradient of the tower features: dxf = dZ_0 W_0^T (no activation)
+    c->bwd_feat = gd(4 * B, c->F, c->enc[0].N, c->dzl[0], c->lddz, false, th + c->enc[0].off,
+                     c->enc[0].ld, true, c->dxf, c->ldf);
+    c->bwd_feat_r = region(c, "enc_bwd_d_0");
+  }
   wgrad(0);
   c->enc_part1 = (int)c->bwd_enc.size();
   wgrad(n);
@@ -295,6 +312,10 @@ static void build_schedule(mvae_ctx* c) {
   for (const char* nm : {"deinterleave", "eps_rng", "latent_fwd", "colsq", "metric_loss", "coldot",
                          "latent_bwd", "adam"})
     region(c, nm);
+  if (c->conv)
+    for (const char* nm : {"conv1_fwd", "conv2_fwd", "lrn2_pool2_fwd", "pool2_bwd", "conv2_wgrad",
+                           "conv2_dgrad", "lrn1_bwd", "conv1_wgrad"})
+      region(c, nm);
 }
 
 static int validate(const mvae_cfg* cfg) {
@@ -312,6 +333,9 @@ static int validate(const mvae_cfg* cfg) {
   if (cfg->precision != MVAE_PREC_F32 && cfg->precision != MVAE_PREC_BF16 &&
       cfg->precision != MVAE_PREC_F32X)
     return fail(nullptr, MVAE_ECONFIG, "bad precision");
+  if (cfg->conv != 0 && cfg->conv != 1) return fail(nullptr, MVAE_ECONFIG, "conv must be 0 or 1");
+  if (cfg->conv && (cfg->image_size % 4 != 0 || cfg->image_size > 400))
+    return fail(nullptr, MVAE_ECONFIG, "conv encoder: image_size must be a multiple of 4 (<= 400)");
   const long long D = (long long)cfg->image_size * cfg->image_size;
   if (D * 3 * cfg->batch > (1LL << 31) - 1 || 3LL * cfg->batch * (D + 4) > (1LL << 31) * 8)
     return fail(nullptr, MVAE_ECONFIG, "batch too large for 32-bit row indexing");
@@ -364,6 +388,18 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   // ---- parameter layout
   size_t off = 0;
   int fan_in = c->D;
+  c->conv = cfg->conv != 0;
+  if (c->conv) {
+    const int S = cfg->image_size;
+    c->tower.S = S; c->tower.S1 = S / 2; c->tower.S2 = S / 4;
+    c->cv1.off = off; c->cv1.K = 25; c->cv1.N = 64; c->cv1.ld = 64;
+    off = align64(off + (size_t)26 * 64);
+    c->cv2.off = off; c->cv2.K = 25 * 64; c->cv2.N = 64; c->cv2.ld = 64;
+    off = align64(off + (size_t)(25 * 64 + 1) * 64);
+    c->F = c->tower.S2 * c->tower.S2 * 64;
+    c->ldf = round8(c->F + 1);
+    fan_in = c->F;
+  }
   for (int i = 0; i < c->nenc; ++i) {
     Block b; b.off = off; b.K = fan_in; b.N = cfg->enc[i]; b.ld = round8(b.N);
     c->enc.push_back(b);
@@ -433,8 +469,37 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   ALLOC(c->dhead, 4 * B * c->ld_dh);
   c->dzl.resize(c->nenc);
   for (int i = 0; i < c->nenc; ++i) ALLOC(c->dzl[i], 4 * B * c->lddz);
+  if (c->conv) {
+    ConvTower& T = c->tower;
+    const size_t a1 = (size_t)T.S1 * T.S1 * 64, a2n = (size_t)T.S2 * T.S2 * 64;
+    T.mfma = cfg->precision == MVAE_PREC_BF16;
+    ALLOC(c->xf, 3 * B * c->ldf);
+    ALLOC(c->dxf, 4 * B * c->ldf);
+    ALLOC(T.p1, 3 * B * a1);
+    ALLOC(T.n1, 3 * B * a1);
+    ALLOC(T.a2, 3 * B * a1);
+    ALLOC(T.da2, 4 * B * a1);
+    ALLOC(T.dn1, 4 * B * a1);
+    float* tmp = nullptr;
+    ALLOC(tmp, (3 * B * a1 + 3) / 4); T.arg1 = reinterpret_cast<unsigned char*>(tmp);
+    ALLOC(tmp, (3 * B * a2n + 3) / 4); T.arg2 = reinterpret_cast<unsigned char*>(tmp);
+    if (T.mfma) {
+      ALLOC(tmp, (3 * B * a1 + 1) / 2); T.n1b = reinterpret_cast<unsigned short*>(tmp);
+      ALLOC(tmp, (4 * B * a1 + 1) / 2); T.da2b = reinterpret_cast<unsigned short*>(tmp);
+      ALLOC(tmp, 25 * 64 * 64 / 2); T.w2f = reinterpret_cast<unsigned short*>(tmp);
+      ALLOC(tmp, 25 * 64 * 64 / 2); T.w2d = reinterpret_cast<unsigned short*>(tmp);
+    }
+    const int B2 = 2 * (int)B;
+    T.nchunk1 = std::min(B2, 256);
+    T.nchunk2 = std::min(B2, 32);
+    T.nchunk2m = std::min(B2, 128);
+    const size_t s1 = (size_t)2 * T.nchunk1 * 26 * 64;
+    const size_t s2 = (size_t)2 * (T.mfma ? T.nchunk2m : T.nchunk2) * (25 * 64 + 1) * 64;
+    ALLOC(T.slab, std::max(s1, s2));
+  }
   // constant ones columns (bias folding)
   hipError_t e = ones_column(c->xs, c->ldx, c->D, 3 * (int)B);
+  if (e == hipSuccess && c->conv) e = ones_column(c->xf, c->ldf, c->F, 3 * (int)B);
   for (int i = 0; e == hipSuccess && i < c->nenc; ++i) e = ones_column(c->H[i], c->ldh[i], cfg->enc[i], 3 * (int)B);
   if (e == hipSuccess) e = ones_column(c->z, c->ldz, c->L, 3 * (int)B);
   if (e == hipSuccess) e = ones_column(c->zgen, c->ldz, c->L, (int)B);
@@ -464,6 +529,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     };
     hipError_t e = add(c->theta, c->n_all);
     if (e == hipSuccess) e = add(c->xs, 3 * B * c->ldx);
+    if (e == hipSuccess && c->conv) e = add(c->xf, 3 * B * c->ldf);
     for (int i = 0; e == hipSuccess && i < c->nenc; ++i) e = add(c->H[i], 3 * B * c->ldh[i]);
     if (e == hipSuccess) e = add(c->z, 3 * B * c->ldz);
     if (e == hipSuccess) e = add(c->zgen, B * c->ldz);
@@ -505,6 +571,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   };
   for (auto* v : {&c->fwd_enc, &c->bwd_dec, &c->bwd_enc})
     for (auto& d : *v) wire(d);
+  if (c->conv) wire(c->bwd_feat);
   wire(c->f_d1);
   wire(c->f_d2);
   wire(c->f_out);
@@ -531,6 +598,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     for (auto* v : {&c->fwd_enc, &c->bwd_dec, &c->bwd_enc})
       for (auto& d : *v) all.push_back(&d);
     for (GemmDesc* d : {&c->f_d1, &c->f_d2, &c->f_out}) all.push_back(d);
+    if (c->conv) all.push_back(&c->bwd_feat);
     for (GemmDesc* d : all) {
       const mvae_ctx::PlaneBuf* pb = nullptr;
       for (const auto& q : c->planes)
@@ -544,6 +612,12 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
       }
       d->epi.c32 = fp32_reader ? 1 : 0;
     }
+  }
+  if (c->conv) {
+    // conv1 reads the fp32 pixels of all three row blocks (forward and weight gradient); the
+    // fp32 feature rows are written only when an fp32 GEMM reads them
+    c->x32mask = 7;
+    c->xf32 = !c->np || c->fwd_enc[0].prec == GEMM_F32 || c->bwd_enc[c->nenc].prec == GEMM_F32;
   }
   for (auto* v : {&c->fwd_enc, &c->bwd_dec, &c->bwd_enc})
     for (auto& d : *v)
@@ -560,6 +634,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   wsz(c->f_d1);
   wsz(c->f_d2);
   wsz(c->f_out);
+  if (c->conv) wsz(c->bwd_feat);
   c->ws_elems = ws;
   if (const char* lg = std::getenv("MVAE_PLAN_LOG"); lg && *lg == '1') {
     // the GEMM plans of this context (diagnostics): shape, arithmetic, kernel, split-K + combine
@@ -596,7 +671,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   return MVAE_OK;
 }
 
-int mvae_param_count(mvae_ctx* ctx) { return ctx ? 2 * ctx->nenc + 4 + 8 : MVAE_EINVAL; }
+int mvae_param_count(mvae_ctx* ctx) { return ctx ? 2 * ctx->nenc + 4 + 8 + (ctx->conv ? 4 : 0) : MVAE_EINVAL; }
 
 int mvae_param_info(mvae_ctx* ctx, int kind, int index, mvae_tensor* out) {
   if (!ctx || !out) return MVAE_EINVAL;
@@ -604,12 +679,22 @@ int mvae_param_info(mvae_ctx* ctx, int kind, int index, mvae_tensor* out) {
   const int count = mvae_param_count(ctx);
   if (index < 0 || index >= count) return fail(ctx, MVAE_EINVAL, "param index out of range");
   std::memset(out, 0, sizeof(*out));
+  const Block* cvb = nullptr;
+  if (ctx->conv) {  // enc_conv1_W, enc_conv1_b, enc_conv2_W, enc_conv2_b come first
+    if (index < 4) cvb = index < 2 ? &ctx->cv1 : &ctx->cv2;
+    else index -= 4;
+  }
   // resolve (name, block-relative pointer) in reference creation order (11a/vae.py:85-153)
   const Block* blk = nullptr;
   bool bias = false;
   int col0 = 0, cols = 0, ld = 0, enc_part = 0;
   std::string name;
-  if (index < 2 * n) {
+  if (cvb) {
+    blk = cvb;
+    bias = index & 1;
+    name = std::string(index < 2 ? "enc_conv1" : "enc_conv2") + (bias ? "_b" : "_W");
+    cols = blk->N; ld = blk->ld; enc_part = 1;
+  } else if (index < 2 * n) {
     const int i = index / 2;
     bias = index & 1;
     blk = &ctx->enc[i];
@@ -771,6 +856,24 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
                              EVAL_STREAM | c->rng_eval++, st));
     }
   }
+  if (c->conv) {  // the tower: xs pixels -> xf features (the FC layer-0 operand)
+    const ConvTower& T = c->tower;
+    const float* w2 = c->theta + c->cv2.off;
+    const int nimg = 3 * c->B;
+    {
+      TIMED("conv1_fwd");
+      MV_CHECK(launch_conv1_fwd(T, c->xs, c->ldx, c->theta + c->cv1.off, nimg, st));
+    }
+    {
+      TIMED("conv2_fwd");
+      if (T.mfma) MV_CHECK(launch_conv2_wprep(T, w2, st));
+      MV_CHECK(launch_conv2(T, true, T.n1, T.n1b, w2, T.w2f, T.a2, nimg, st));
+    }
+    {
+      TIMED("lrn2_pool2_fwd");
+      MV_CHECK(launch_lrn2_pool2_fwd(T, nimg, c->xf, c->ldf, c->xf32, planes_of(c, c->xf), st));
+    }
+  }
   for (size_t i = 0; i < c->fwd_enc.size(); ++i) {
     int rc = run(c, c->fwd_enc[i], st, c->fwd_enc_r[i]);
     if (rc) return rc;
@@ -878,6 +981,32 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
       }
     }
     if ((rc = run(c, c->bwd_enc[n], st, c->bwd_enc_r[n]))) return rc;  // wgrad(0)
+    if (c->conv) {  // back through the tower (its gradients are final at the end of part 1)
+      const ConvTower& T = c->tower;
+      float* g1 = c->grads;
+      float* g2 = c->grads + c->n_all;
+      if ((rc = run(c, c->bwd_feat, st, c->bwd_feat_r))) return rc;
+      {
+        TIMED("pool2_bwd");
+        MV_CHECK(launch_pool2_bwd(T, c->dxf, c->ldf, c->B, st));
+      }
+      {
+        TIMED("conv2_wgrad");
+        MV_CHECK(launch_conv2_wgrad(T, c->B, g1 + c->cv2.off, g2 + c->cv2.off, st));
+      }
+      {
+        TIMED("conv2_dgrad");
+        MV_CHECK(launch_conv2(T, false, T.da2, T.da2b, c->theta + c->cv2.off, T.w2d, T.dn1, 4 * c->B, st));
+      }
+      {
+        TIMED("lrn1_bwd");
+        MV_CHECK(launch_lrn1_bwd(T, c->B, st));
+      }
+      {
+        TIMED("conv1_wgrad");
+        MV_CHECK(launch_conv1_wgrad(T, c->xs, c->ldx, c->B, g1 + c->cv1.off, g2 + c->cv1.off, st));
+      }
+    }
     ctx->phase = 5;
   } else {
     if ((rc = join())) return rc;
@@ -1240,6 +1369,61 @@ extern "C" int mvae_make_batch(const unsigned char* locks, const unsigned char* 
     return fail(nullptr, MVAE_EINVAL, "mvae_make_batch: coef must be 16-byte aligned");
   hipError_t e = launch_make_batch(locks, keys, height, width, idx, coef, batch, divisor, x_out,
                                    (hipStream_t)stream);
+  if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
+  return MVAE_OK;
+}
+
+// One conv2 kernel of the conv tower on caller data (tests only; synchronous): S1 x S1 x 64
+// images, B = batch (3B forward images, 4B backward images). mode 0: out = relu(conv(x, W) + b)
+// over 3B images (y = W2 block [1601][64]); mode 1: out = data gradient conv(x, W rotated) over
+// 4B images (y = W2); mode 2: out[2][1601][64] = the two weight gradients of x = n1 (3B) and
+// y = d a2 (4B). mfma: the bf16 MFMA kernels (operands rounded to bf16) instead of fp32 VALU.
+extern "C" int mvae_debug_conv2(int S1, int B, int mode, int mfma, const float* x, const float* y,
+                                float* out, void* stream) {
+  if (S1 <= 0 || S1 > 200 || B <= 0 || mode < 0 || mode > 2 || !x || !y || !out)
+    return fail(nullptr, MVAE_EINVAL, "mvae_debug_conv2: bad argument");
+  hipStream_t st = (hipStream_t)stream;
+  ConvTower T;
+  T.S1 = S1; T.S = 2 * S1; T.S2 = S1 / 2;
+  T.mfma = mfma != 0;
+  const size_t img = (size_t)S1 * S1 * 64;
+  const int B2 = 2 * B;
+  T.nchunk2 = std::min(B2, 32);
+  T.nchunk2m = std::min(B2, 128);
+  std::vector<void*> tmp;
+  hipError_t e = hipSuccess;
+  auto alloc = [&](size_t bytes) -> void* {
+    void* p = nullptr;
+    if (e == hipSuccess) e = hipMalloc(&p, std::max<size_t>(bytes, 4));
+    if (e == hipSuccess) tmp.push_back(p);
+    return p;
+  };
+  auto bf16_of = [&](const float* src, size_t n) -> unsigned short* {
+    unsigned short* p = static_cast<unsigned short*>(alloc(n * 2));
+    if (e == hipSuccess) e = launch_split_planes(src, n, Planes{p, (long long)n, 1}, st);
+    return p;
+  };
+  if (mode == 2) {
+    T.n1 = const_cast<float*>(x);
+    T.da2 = const_cast<float*>(y);
+    const size_t ns = (size_t)2 * (T.mfma ? T.nchunk2m : T.nchunk2) * (25 * 64 + 1) * 64;
+    T.slab = static_cast<float*>(alloc(ns * 4));
+    if (T.mfma) { T.n1b = bf16_of(x, 3 * B * img); T.da2b = bf16_of(y, 4 * B * img); }
+    if (e == hipSuccess) e = launch_conv2_wgrad(T, B, out, out + (size_t)(25 * 64 + 1) * 64, st);
+  } else {
+    const int nimg = mode == 0 ? 3 * B : 4 * B;
+    const unsigned short* xb = nullptr;
+    if (T.mfma) {
+      xb = bf16_of(x, nimg * img);
+      T.w2f = static_cast<unsigned short*>(alloc(25 * 64 * 64 * 2));
+      T.w2d = static_cast<unsigned short*>(alloc(25 * 64 * 64 * 2));
+      if (e == hipSuccess) e = launch_conv2_wprep(T, y, st);
+    }
+    if (e == hipSuccess)
+      e = launch_conv2(T, mode == 0, x, xb, y, mode == 0 ? T.w2f : T.w2d, out, nimg, st);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  for (void* p : tmp) (void)hipFree(p);
   if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
   return MVAE_OK;
 }

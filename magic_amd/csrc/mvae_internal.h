@@ -130,6 +130,47 @@ hipError_t launch_split_planes(const float* src, size_t n, const Planes& dst, hi
 hipError_t launch_make_batch(const unsigned char* locks, const unsigned char* keys, int H, int W,
                              const int* idx, const float* coef, int B, float div, float* x,
                              hipStream_t st);
+// ---- conv-encoder tower (conv_tower.hip, conv_mfma.hip) ----
+// NHWC fp32 activations of the stacked batch (3B forward rows, 4B backward rows); S = image
+// side, S1 = S/2 (after pool 1), S2 = S/4 (after pool 2).
+struct ConvTower {
+  int S = 0, S1 = 0, S2 = 0;
+  float* p1 = nullptr;             // pool-1 output        [3B][S1*S1][64]
+  unsigned char* arg1 = nullptr;   // its window argmax    [3B][S1*S1][64]
+  float* n1 = nullptr;             // LRN-1 output = conv2 input
+  unsigned short* n1b = nullptr;   // ... bf16 (MFMA mode)
+  float* a2 = nullptr;             // conv2 + ReLU output  [3B][S1*S1][64]
+  unsigned char* arg2 = nullptr;   // pool-2 window argmax [3B][S2*S2][64]
+  float* da2 = nullptr;            // d conv2 pre-activation [4B][S1*S1][64]
+  unsigned short* da2b = nullptr;  // ... bf16 (MFMA mode)
+  float* dn1 = nullptr;            // d LRN-1 output, then (in place) d conv1 pooled pre-activation
+  unsigned short *w2f = nullptr, *w2d = nullptr;  // bf16 conv2 kernel images [25][64 n][64 k]
+  float* slab = nullptr;           // weight-gradient partial sums (fixed-order reduction)
+  int nchunk1 = 1, nchunk2 = 1, nchunk2m = 1;
+  bool mfma = false;               // conv2 on bf16 MFMA (bf16 mode)
+};
+hipError_t launch_conv1_fwd(const ConvTower& T, const float* xs, int ldx, const float* w1, int nimg,
+                            hipStream_t st);
+// fwd: a2 = relu(conv(n1, W2) + b2) over nimg images; !fwd: dn1 = conv_dgrad(da2, W2)
+hipError_t launch_conv2(const ConvTower& T, bool fwd, const float* in, const unsigned short* inb,
+                        const float* w2, const unsigned short* w2b, float* out, int nimg, hipStream_t st);
+hipError_t launch_lrn2_pool2_fwd(const ConvTower& T, int nimg, float* xf, int ldf, int f32,
+                                 const Planes& xfp, hipStream_t st);
+hipError_t launch_pool2_bwd(const ConvTower& T, const float* dxf, int ldf, int B, hipStream_t st);
+hipError_t launch_lrn1_bwd(const ConvTower& T, int B, hipStream_t st);
+hipError_t launch_conv1_wgrad(const ConvTower& T, const float* xs, int ldx, int B, float* g1, float* g2,
+                              hipStream_t st);
+hipError_t launch_conv2_wgrad(const ConvTower& T, int B, float* g1, float* g2, hipStream_t st);
+hipError_t launch_conv2_wprep(const ConvTower& T, const float* w2, hipStream_t st);
+hipError_t launch_conv2_mfma(const ConvTower& T, bool fwd, const unsigned short* inb,
+                             const unsigned short* wimg, const float* w2, float* out, int nimg,
+                             hipStream_t st);
+hipError_t launch_conv2_wgrad_mfma(const ConvTower& T, int B, hipStream_t st);
+int conv2_mfma_band(int S1);
+size_t conv2_mfma_lds(int S1);
+int conv2_wgrad_rows(int S1);
+size_t conv2_wgrad_lds(int S1);
+
 // empty kernel of MARKER_GRID + region workgroups (64 threads): a region boundary that a
 // rocprofv3 kernel trace shows (counter passes attribute the dispatches between two markers)
 constexpr int MARKER_GRID = 4096;

@@ -54,6 +54,7 @@ class Engine:
         c.beta1, c.beta2, c.epsilon = cfg.beta1, cfg.beta2, cfg.epsilon
         c.precision = _lib.PREC[cfg.precision]
         c.seed = cfg.seed
+        c.conv = int(getattr(cfg, "conv", False))
         torch.cuda.set_device(device)
         torch.cuda.init()
         h = C.c_void_p()
@@ -143,6 +144,8 @@ class Engine:
         for name, v in views.items():
             if v.dim() == 2:
                 fan_in, fan_out = v.shape
+                if name.startswith("enc_conv"):  # slim xavier: receptive field on both fans
+                    fan_out *= 25
                 hi = np.sqrt(6.0 / (fan_in + fan_out))
                 v.copy_(torch.from_numpy(rng.uniform(-hi, hi, size=(fan_in, fan_out)).astype(np.float32)).to(self.dev))
             else:

@@ -47,6 +47,8 @@ from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
 
+from . import conv_oracle as CV
+
 L2_EPS = 1e-12  # tf.nn.l2_normalize default epsilon
 
 
@@ -64,6 +66,7 @@ class OracleConfig:
     beta1: float = 0.9
     beta2: float = 0.999
     epsilon: float = 1e-8
+    conv: bool = False           # conv-encoder variant (conv_oracle.py)
 
     @property
     def D(self) -> int:
@@ -76,6 +79,9 @@ def param_shapes(cfg) -> List[Tuple[str, Tuple[int, ...]]]:
     D, L = cfg.D, cfg.latent
     out = []
     fan_in = D
+    if getattr(cfg, "conv", False):  # the CifarNet tower comes first (encoder variables)
+        out += CV.param_shapes()
+        fan_in = CV.feat_dim(cfg.image_size)
     for i, e in enumerate(cfg.enc):
         out.append((f"enc_h{i}_W", (fan_in, e)))
         out.append((f"enc_h{i}_b", (e,)))
@@ -110,7 +116,12 @@ def init_params(cfg, seed: int = 0, dtype=np.float32) -> Dict[str, np.ndarray]:
     rng = np.random.default_rng(seed)
     P = {}
     for name, shp in param_shapes(cfg):
-        P[name] = xavier_init(rng, *shp, dtype=dtype) if len(shp) == 2 else np.zeros(shp, dtype)
+        if len(shp) == 2:
+            fi, fo = CV.xavier_fans(name, shp)
+            hi = np.sqrt(6.0 / (fi + fo))
+            P[name] = rng.uniform(-hi, hi, size=shp).astype(dtype)
+        else:
+            P[name] = np.zeros(shp, dtype)
     return P
 
 
@@ -139,7 +150,12 @@ def split_input(X, cfg):
 
 
 def encode(P, x, cfg):
-    """``get_latent_representation`` ``11a/vae.py:335-367`` without the sampling."""
+    """``get_latent_representation`` ``11a/vae.py:335-367`` without the sampling. With
+    ``cfg.conv`` the FC layers read the conv tower's features (hs[0]); the tower's cache is
+    returned as the 4th value (None otherwise)."""
+    tc = None
+    if getattr(cfg, "conv", False):
+        x, tc = CV.tower_forward(P, x, cfg.image_size)
     hs = [x]
     h = x
     for i in range(len(cfg.enc)):
@@ -147,7 +163,7 @@ def encode(P, x, cfg):
         hs.append(h)
     mu = h @ P["enc_out_mean_W"] + P["enc_out_mean_b"]
     s = h @ P["enc_out_log_sigma_W"] + P["enc_out_log_sigma_b"]
-    return hs, mu, s
+    return hs, mu, s, tc
 
 
 def decode(P, z, cfg):
@@ -178,10 +194,10 @@ def forward(P, X, eps, cfg, dtype=np.float64):
     xl, xr, xk = split_input(X, cfg)
     c = {"P": P, "xl": xl, "eps": eps}
     for tag, x, e in (("l", xl, eps[0]), ("r", xr, eps[1]), ("k", xk, eps[2])):
-        hs, mu, s = encode(P, x, cfg)
+        hs, mu, s, tc = encode(P, x, cfg)
         sig = np.sqrt(np.exp(s))                       # tf.sqrt(tf.exp(s)), 11a/vae.py:376
         z = mu + sig * e
-        c.update({f"hs_{tag}": hs, f"mu_{tag}": mu, f"s_{tag}": s, f"sig_{tag}": sig, f"z_{tag}": z})
+        c.update({f"tc_{tag}": tc, f"hs_{tag}": hs, f"mu_{tag}": mu, f"s_{tag}": s, f"sig_{tag}": sig, f"z_{tag}": z})
     d1, d2, u, y = decode(P, c["z_l"], cfg)
     c.update(d1=d1, d2=d2, u=u, y=y)
     c["R"] = bce_rows(y, xl)                                                   # 11a/vae.py:266-269
@@ -226,7 +242,7 @@ def loss_sums(c, B_global: int):
     return np.array([R + K + F, T, R, K, F])
 
 
-def _enc_backward(P, hs, dmu, ds, cfg, acc: Dict[str, np.ndarray], mag: bool = False):
+def _enc_backward(P, hs, dmu, ds, cfg, acc: Dict[str, np.ndarray], mag: bool = False, tc=None):
     A = np.abs if mag else (lambda v: v)
     h = A(hs[-1])
     for nm, d in (("enc_out_mean", dmu), ("enc_out_log_sigma", ds)):
@@ -237,8 +253,10 @@ def _enc_backward(P, hs, dmu, ds, cfg, acc: Dict[str, np.ndarray], mag: bool = F
         dz = A(act_grad(hs[i + 1], dh, cfg.act))
         acc[f"enc_h{i}_W"] = acc.get(f"enc_h{i}_W", 0) + A(hs[i]).T @ dz
         acc[f"enc_h{i}_b"] = acc.get(f"enc_h{i}_b", 0) + dz.sum(0)
-        if i > 0:
+        if i > 0 or tc is not None:
             dh = dz @ A(P[f"enc_h{i}_W"]).T
+    if tc is not None:  # through the conv tower (dh = dL/d features)
+        CV.tower_backward(P, tc, dh, acc, mag)
     return acc
 
 
@@ -281,8 +299,8 @@ def backward(c, cfg, B_global: int, coldot_global=None, magnitude: bool = False)
         dmu_l1 = dzl1 + c["mu_l"] * inv
         ds_l1 = 0.5 * dzl1 * el * c["sig_l"] + 0.5 * (np.exp(c["s_l"]) - 1) * inv
     dmu_r1, ds_r1 = A(dzr1), A(0.5 * dzr1 * er * c["sig_r"])
-    _enc_backward(P, c["hs_l"], A(dmu_l1), A(ds_l1), cfg, g1, magnitude)
-    _enc_backward(P, c["hs_r"], dmu_r1, ds_r1, cfg, g1, magnitude)
+    _enc_backward(P, c["hs_l"], A(dmu_l1), A(ds_l1), cfg, g1, magnitude, c.get("tc_l"))
+    _enc_backward(P, c["hs_r"], dmu_r1, ds_r1, cfg, g1, magnitude, c.get("tc_r"))
     # metric (g2)
     draw = A(c["draw"][:, None])
     if cfg.metric == "sqdiff":
@@ -300,8 +318,8 @@ def backward(c, cfg, B_global: int, coldot_global=None, magnitude: bool = False)
             dzl2 = c["rl"] * (draw * c["nk"] - c["nl"] * cd * ml)
             dzk2 = c["rk"] * (draw * c["nl"] - c["nk"] * cd * mk)
     g2: Dict[str, np.ndarray] = {}
-    _enc_backward(P, c["hs_l"], dzl2, A(0.5 * dzl2 * el * c["sig_l"]), cfg, g2, magnitude)
-    _enc_backward(P, c["hs_k"], dzk2, A(0.5 * dzk2 * ek * c["sig_k"]), cfg, g2, magnitude)
+    _enc_backward(P, c["hs_l"], dzl2, A(0.5 * dzl2 * el * c["sig_l"]), cfg, g2, magnitude, c.get("tc_l"))
+    _enc_backward(P, c["hs_k"], dzk2, A(0.5 * dzk2 * ek * c["sig_k"]), cfg, g2, magnitude, c.get("tc_k"))
     return g1, g2
 
 

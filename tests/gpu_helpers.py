@@ -14,7 +14,8 @@ def oracle_cfg(cfg: MVAEConfig) -> O.OracleConfig:
     return O.OracleConfig(image_size=cfg.image_size, enc=tuple(cfg.enc), dec=tuple(cfg.dec),
                           latent=cfg.latent, act=cfg.act, deform_weight=cfg.deform_weight,
                           metric=cfg.metric, reciprocal=cfg.reciprocal, lr=tuple(cfg.lr),
-                          beta1=cfg.beta1, beta2=cfg.beta2, epsilon=cfg.epsilon)
+                          beta1=cfg.beta1, beta2=cfg.beta2, epsilon=cfg.epsilon,
+                          conv=getattr(cfg, "conv", False))
 
 
 def make_inputs(cfg: MVAEConfig, B: int, seed: int = 1, density: float = 0.1, grey: bool = False):

@@ -1,0 +1,163 @@
+"""Conv-encoder variant (BASELINE config 5) on the HIP path vs the oracle
+(oracle/conv_oracle.py, itself pinned against torch.autograd in tests/test_conv_oracle.py;
+parity with the reference is unpinned by nature: the reference has no conv VAE).
+
+f32 / f32x (tower in fp32 VALU kernels): the north-star bar, 1e-4 max-norm relative per
+tensor, cancellation-aware as in test_gpu_parity.py. bf16 (tower conv2 on bf16 MFMA,
+fp32 accumulate): the documented bf16 tolerance of test_gpu_parity.py (losses 2e-3,
+distance 2e-2, gradients 5e-2)."""
+import numpy as np
+import pytest
+import torch
+
+from magic_amd.config import MVAEConfig, preset
+from oracle import mvae_oracle as O
+from tests.gpu_helpers import gpu_phases, make_inputs, make_params, oracle_cfg, to_dev
+from tests.test_gpu_parity import FLAVOURS, _engine, check_step
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+def tiny_conv(act, metric, recip, w, **kw):
+    base = dict(image_size=12, batch=6, enc=(40, 24), dec=(28, 20), latent=6, act=act,
+                metric=metric, reciprocal=recip, deform_weight=w, lr=(1e-3, 1e-4), conv=True)
+    base.update(kw)
+    return MVAEConfig(**base)
+
+
+@pytest.mark.parametrize("flav", FLAVOURS)
+def test_conv_step_f32(flav):
+    check_step(tiny_conv(*flav), density=0.3)
+
+
+@pytest.mark.parametrize("S,B", [(20, 4), (16, 9)])
+def test_conv_step_f32_sizes(S, B):
+    check_step(tiny_conv("tanh", "sqdiff", True, 10.0, image_size=S, batch=B), density=0.3)
+
+
+def test_conv_step_f32x():
+    check_step(tiny_conv("tanh", "cosine", False, 10.0, image_size=20, batch=4, precision="f32x"),
+               density=0.3)
+
+
+@pytest.mark.parametrize("S,B", [(12, 6), (20, 4), (100, 2)])
+def test_conv_step_bf16_mfma(S, B):
+    """conv2 forward / data gradient / weight gradient on the bf16 MFMA kernels."""
+    cfg = tiny_conv("tanh", "sqdiff", True, 10.0, image_size=S, batch=B, precision="bf16",
+                    enc=(500, 64) if S == 100 else (40, 24))
+    check_step(cfg, density=0.3, tol=5e-2, loss_tol=2e-3, dist_tol=2e-2, adam=False)
+
+
+def test_conv_full_image_f32():
+    """100x100 images (the benched geometry: 50x50x64 after pool 1, 40000 features)."""
+    check_step(tiny_conv("tanh", "sqdiff", True, 10.0, image_size=100, batch=2, enc=(64,)),
+               density=0.3, adam=False)
+
+
+def test_conv_step_deterministic():
+    cfg = tiny_conv("tanh", "cosine", False, 10.0, image_size=20, batch=8, precision="bf16")
+    out = []
+    for _ in range(2):
+        eng = _engine(cfg)
+        try:
+            eng.load_params(make_params(cfg))
+            X, areas, eps = make_inputs(cfg, cfg.batch, density=0.3)
+            _, _, g1, g2 = gpu_phases(eng, X, areas, eps)
+            out.append((g1, g2))
+        finally:
+            eng.close()
+    for k in out[0][0]:
+        np.testing.assert_array_equal(out[0][0][k], out[1][0][k], err_msg=k)
+
+
+def test_conv_transform_matches_oracle():
+    cfg = tiny_conv("elu", "cosine", False, 100.0, image_size=16, batch=5)
+    eng = _engine(cfg)
+    try:
+        P = make_params(cfg)
+        eng.load_params(P)
+        X, _, _ = make_inputs(cfg, cfg.batch, density=0.3)
+        mu = eng.transform(to_dev(X)).cpu().numpy()
+        oc = oracle_cfg(cfg)
+        _, mu_o, _, _ = O.encode({k: v.astype(np.float64) for k, v in P.items()},
+                                 X[:, 0::3].astype(np.float64), oc)
+        assert np.abs(mu - mu_o).max() <= 1e-4 * np.abs(mu_o).max()
+        names = list(eng.params())
+        assert names[:4] == ["enc_conv1_W", "enc_conv1_b", "enc_conv2_W", "enc_conv2_b"]
+        assert tuple(eng.params()["enc_conv2_W"].shape) == (1600, 64)
+    finally:
+        eng.close()
+
+
+def test_conv_c5conv_preset_runs():
+    """The benched configuration's shape (C5CONV: 8e encoder, L=2000, conv tower) at a batch
+    the oracle handles: bf16 tolerance."""
+    cfg = preset("8e", image_size=100, batch=4, metric="sqdiff", reciprocal=True,
+                 precision="bf16", conv=True)
+    check_step(cfg, density=0.1, tol=5e-2, loss_tol=2e-3, dist_tol=2e-2, adam=False)
+
+
+# ------------------------------------------------------------------ conv2 kernels in isolation
+def _bf16(a):
+    u = np.ascontiguousarray(a, np.float32).view(np.uint32).astype(np.uint64)
+    u = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return u.astype(np.uint32).view(np.float32)
+
+
+def _conv2_ref(mode, x, y, S1, B):
+    """float64 restatement with the kernel's operand rounding already applied to x, y."""
+    from oracle import conv_oracle as CV
+    x = x.astype(np.float64).reshape(-1, S1, S1, 64)
+    y = y.astype(np.float64)
+    if mode == 0:
+        return np.maximum(CV.conv(x, y[:1600], y[1600]), 0), CV.conv(np.abs(x), np.abs(y[:1600]), 0)
+    if mode == 1:
+        Wr = CV.rot_weights(y[:1600], 64)
+        return CV.im2col(x) @ Wr, CV.im2col(np.abs(x)) @ np.abs(Wr)
+    d = y.reshape(-1, S1, S1, 64)
+    out, mag = [], []
+    for g in range(2):
+        rows = np.arange(2 * B) + 2 * B * g
+        fwd = np.where(rows < 2 * B, rows, rows - B)
+        cols = CV.im2col(x[fwd]).reshape(-1, 1600)
+        dd = d[rows].reshape(-1, 64)
+        w = np.concatenate([cols.T @ dd, dd.sum(0)[None]], 0)
+        m = np.concatenate([np.abs(cols).T @ np.abs(dd), np.abs(dd).sum(0)[None]], 0)
+        out.append(w)
+        mag.append(m)
+    return np.stack(out), np.stack(mag)
+
+
+@pytest.mark.parametrize("mfma", [0, 1], ids=["valu_f32", "mfma_bf16"])
+@pytest.mark.parametrize("mode", [0, 1, 2], ids=["fwd", "dgrad", "wgrad"])
+@pytest.mark.parametrize("S1,B", [(6, 2), (10, 3), (50, 1)])
+def test_conv2_kernel(mode, mfma, S1, B):
+    from magic_amd import _lib
+    lib = _lib.load()
+    rng = np.random.default_rng(S1 * 10 + mode)
+    img = S1 * S1 * 64
+    nx = (3 * B if mode in (0, 2) else 4 * B) * img
+    x = np.maximum(rng.standard_normal(nx), -0.2).astype(np.float32)   # relu-ish, with zeros
+    if mode == 2:
+        y = (rng.standard_normal(4 * B * img) * (rng.random(4 * B * img) < 0.3)).astype(np.float32)
+        out = torch.zeros(2 * 1601 * 64, device="cuda")
+    else:
+        y = (rng.standard_normal(1601 * 64) * 0.05).astype(np.float32)
+        out = torch.zeros((3 * B if mode == 0 else 4 * B) * img, device="cuda")
+    xd, yd = to_dev(x), to_dev(y)
+    rc = lib.mvae_debug_conv2(S1, B, mode, mfma, xd.data_ptr(), yd.data_ptr(), out.data_ptr(),
+                              torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, lib.mvae_last_error(None)
+    xr, yr = (_bf16(x), _bf16(y)) if mfma else (x, y)
+    if mfma and mode != 2:
+        yr = np.concatenate([_bf16(y[:1600 * 64]), y[1600 * 64:]])   # the bias stays fp32
+    ref, mag = _conv2_ref(mode, xr, yr, S1, B)
+    got = out.cpu().numpy().astype(np.float64).reshape(ref.shape)
+    err = np.abs(got - ref).max() / max(np.abs(mag).max(), 1e-30)
+    assert err <= 2e-6, err

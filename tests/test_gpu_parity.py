@@ -365,7 +365,7 @@ def test_inference_surface_matches_oracle():
         dist = eng.predict(x, to_dev(eps)).cpu().numpy()
         assert max_rel(dist, O.predictions(P, X, eps, oc)) <= TOL
         zm = eng.transform(x).cpu().numpy()
-        _, mu, _ = O.encode({k: v.astype(np.float64) for k, v in P.items()}, X[:, 0::3].astype(np.float64), oc)
+        _, mu, _, _ = O.encode({k: v.astype(np.float64) for k, v in P.items()}, X[:, 0::3].astype(np.float64), oc)
         assert max_rel(zm, mu) <= TOL
         y = eng.reconstruct(x, to_dev(eps)).cpu().numpy()
         c = O.forward(P, X, eps, oc)
