@@ -93,8 +93,16 @@ def self_launch(args, argv) -> int:
 def region_flops(cfg, name: str) -> float:
     """Algorithmic FLOPs of one launch of a timed GEMM region (2*M*N*K, K = fan-in)."""
     B, D, L = cfg.batch, cfg.D, cfg.latent
-    widths = [D] + list(cfg.enc)
+    S1 = cfg.image_size // 2
+    F0 = (S1 // 2) ** 2 * 64 if cfg.conv else D   # layer-0 fan-in: pixels or tower features
+    widths = [F0] + list(cfg.enc)
     e, (d0, d1) = cfg.enc[-1], cfg.dec
+    if cfg.conv:  # the 5x5x64x64 conv as an implicit GEMM (K = 25 taps x 64 channels)
+        conv2 = 2.0 * S1 * S1 * 1600 * 64
+        if name == "conv2_fwd":
+            return 3 * B * conv2
+        if name in ("conv2_dgrad", "conv2_wgrad"):
+            return 4 * B * conv2
     if name.startswith("enc_fwd_"):
         i = int(name.rsplit("_", 1)[1])
         return 2.0 * 3 * B * widths[i] * widths[i + 1]
@@ -145,6 +153,21 @@ def region_bytes(cfg, name: str) -> float:
         return 2 * BL * 4.0 + B * 4.0
     if name == "latent_bwd":    # z (3 blocks), mu/s (3 blocks), eps (3), dz_dec in; dhead (4 rows x 2L) out
         return BL * (12.0 + 24.0 + 12.0 + 4.0) + 4 * BL * 2 * (4.0 + 2.0 * np_)
+    if cfg.conv:  # the conv tower's per-pixel kernels (magic_amd/csrc/conv_tower.hip)
+        S1 = cfg.image_size // 2
+        A1 = S1 * S1 * 64.0                # elements of one image after pool 1
+        F = (S1 // 2) ** 2 * 64.0          # tower features
+        mf = 2.0 if cfg.precision == "bf16" else 0.0   # bf16 copies for the MFMA conv
+        if name == "conv1_fwd":         # pixels in; p1, arg1, n1 (+ bf16 n1) out
+            return 3 * B * (D * 4.0 + A1 * (9.0 + mf))
+        if name == "lrn2_pool2_fwd":    # a2 in; features (fp32 and/or planes) + arg2 out
+            return 3 * B * (A1 * 4.0 + F * (4.0 + 2.0 * np_ + 1.0))
+        if name == "pool2_bwd":         # dxf, arg2, a2 in; d a2 (+ bf16) out, per backward image
+            return 4 * B * (F * 5.0 + A1 * (8.0 + mf))
+        if name == "lrn1_bwd":          # d, p1 in; d out (in place)
+            return 4 * B * A1 * 12.0
+        if name == "conv1_wgrad":       # d, arg1, pixels in
+            return 4 * B * (A1 * 5.0 + D * 4.0)
     return 0.0
 
 
@@ -275,8 +298,9 @@ def cpu_baseline(cfg, dev, seconds: float):
 
     oc = O.OracleConfig(image_size=cfg.image_size, enc=tuple(cfg.enc), dec=tuple(cfg.dec),
                         latent=cfg.latent, act=cfg.act, deform_weight=cfg.deform_weight,
-                        metric=cfg.metric, reciprocal=cfg.reciprocal, lr=tuple(cfg.lr))
-    B1 = 64
+                        metric=cfg.metric, reciprocal=cfg.reciprocal, lr=tuple(cfg.lr),
+                        conv=cfg.conv)
+    B1 = 8 if cfg.conv else 64   # the conv oracle's im2col: 3*B*2500 x 1600 per step
     c1 = cfg.replace(batch=B1, global_batch=B1)
     x1, a1 = synthetic_batch(B1, cfg.image_size, seed=4242, device=dev)
     eps1 = torch.from_numpy(np.random.default_rng(2).standard_normal((3, B1, cfg.latent))
@@ -582,7 +606,8 @@ def main():
             n_enc = eng.buffer(_lib.BUF_GRADS).numel() - n_all
             np_ = {"f32": 0, "bf16": 1, "f32x": 3}[cfg.precision]
             for k in ("deinterleave", "eps_rng", "latent_fwd", "colsq", "metric_loss", "coldot",
-                      "latent_bwd", "adam"):
+                      "latent_bwd", "adam", "conv1_fwd", "lrn2_pool2_fwd", "pool2_bwd", "lrn1_bwd",
+                      "conv1_wgrad"):
                 if k not in regions:
                     continue
                 ms_k = regions[k][0] / regions[k][1]
@@ -650,7 +675,8 @@ def main():
                      "synthetic 100x100 binary shape pairs (random ellipses/rectangles, nearest-"
                      "neighbour rotated lock), areas resampled from the reference's OVERLAP_AREAS; "
                      "random xavier init"),
-            "config": {"workload": f"BASELINE {args.config}: preset "
+            "config": {"workload": f"BASELINE {args.config}: "
+                                   f"{'CifarNet conv tower (6b/net.py:50-60) + ' if cfg.conv else ''}preset "
                                    f"{ {20: '8c', 200: '8d', 2000: '8e'}.get(cfg.latent, '?') } enc "
                                    f"{list(cfg.enc)} L={cfg.latent} {cfg.act} "
                                    f"{'reciprocal ' if cfg.reciprocal else ''}{cfg.metric}",

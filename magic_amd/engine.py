@@ -147,7 +147,7 @@ class Engine:
                 if name.startswith("enc_conv"):  # slim xavier: receptive field on both fans
                     fan_out *= 25
                 hi = np.sqrt(6.0 / (fan_in + fan_out))
-                v.copy_(torch.from_numpy(rng.uniform(-hi, hi, size=(fan_in, fan_out)).astype(np.float32)).to(self.dev))
+                v.copy_(torch.from_numpy(rng.uniform(-hi, hi, size=tuple(v.shape)).astype(np.float32)).to(self.dev))
             else:
                 v.zero_()
         self.sync_params()
