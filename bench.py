@@ -157,17 +157,15 @@ def region_bytes(cfg, name: str) -> float:
         S1 = cfg.image_size // 2
         A1 = S1 * S1 * 64.0                # elements of one image after pool 1
         F = (S1 // 2) ** 2 * 64.0          # tower features
-        mf = 2.0 if cfg.precision == "bf16" else 0.0   # bf16 copies for the MFMA conv
-        if name == "conv1_fwd":         # pixels in; p1, arg1, n1 (+ bf16 n1) out
-            return 3 * B * (D * 4.0 + A1 * (9.0 + mf))
+        mf = cfg.precision == "bf16"    # MFMA conv: bf16 n1 / d a2 images instead of fp32
+        if name == "conv1_fwd":         # pixels in; p1, arg1, n1 (fp32 or bf16) out
+            return 3 * B * (D * 4.0 + A1 * (5.0 + (2.0 if mf else 4.0)))
         if name == "lrn2_pool2_fwd":    # a2 in; features (fp32 and/or planes) + arg2 out
             return 3 * B * (A1 * 4.0 + F * (4.0 + 2.0 * np_ + 1.0))
-        if name == "pool2_bwd":         # dxf, arg2, a2 in; d a2 (+ bf16) out, per backward image
-            return 4 * B * (F * 5.0 + A1 * (8.0 + mf))
-        if name == "lrn1_bwd":          # d, p1 in; d out (in place)
-            return 4 * B * A1 * 12.0
-        if name == "conv1_wgrad":       # d, arg1, pixels in
-            return 4 * B * (A1 * 5.0 + D * 4.0)
+        if name == "pool2_bwd":         # dxf, arg2, a2 in; d a2 (fp32 or bf16) out, per backward image
+            return 4 * B * (F * 5.0 + A1 * (4.0 + (2.0 if mf else 4.0)))
+        if name == "conv1_wgrad":       # d n1, p1, arg1, pixels in (LRN-1 backward fused)
+            return 4 * B * (A1 * 9.0 + D * 4.0)
     return 0.0
 
 
@@ -606,8 +604,7 @@ def main():
             n_enc = eng.buffer(_lib.BUF_GRADS).numel() - n_all
             np_ = {"f32": 0, "bf16": 1, "f32x": 3}[cfg.precision]
             for k in ("deinterleave", "eps_rng", "latent_fwd", "colsq", "metric_loss", "coldot",
-                      "latent_bwd", "adam", "conv1_fwd", "lrn2_pool2_fwd", "pool2_bwd", "lrn1_bwd",
-                      "conv1_wgrad"):
+                      "latent_bwd", "adam", "conv1_fwd", "lrn2_pool2_fwd", "pool2_bwd", "conv1_wgrad"):
                 if k not in regions:
                     continue
                 ms_k = regions[k][0] / regions[k][1]

@@ -138,10 +138,12 @@ __global__ __launch_bounds__(256, 2) void conv2_mfma_kernel(const unsigned short
   }
 }
 
-// Weight gradient. Grid: 8 * ceil(2 * nchunk * 4 / 8) workgroups; id -> (XCD = id & 7,
+// Weight gradient. The next row block's operand rows are fetched into registers (NA + 4 16-B
+// chunks per thread) while the current block computes. Grid: 8 * ceil(2 * nchunk * 4 / 8) workgroups; id -> (XCD = id & 7,
 // sibling s = (id >> 3) & 3 = k half * 2 + n half, chunk group). LDS: the image rows of one row
 // block [r0, r0 + R) for one channel half: A patch (R+4) x (S1+4) x 32 and d 16*nk x 32 (64-B
 // pixel rows: four consecutive pixels of a tr16 group span the 256-B bank row, no swizzle).
+template <int NA>
 __global__ __launch_bounds__(256, 2) void conv2_wgrad_mfma_kernel(const unsigned short* __restrict__ inb,
                                                                   const unsigned short* __restrict__ db,
                                                                   int S1, int R, int B2, int nchunk, int ipc,
@@ -160,6 +162,9 @@ __global__ __launch_bounds__(256, 2) void conv2_wgrad_mfma_kernel(const unsigned
   const int j0 = grp * B2 + chunk * ipc;
   const int j1 = min(j0 + ipc, grp * B2 + B2);
   const int np1 = S1 * S1;
+  const int nrb = (S1 + R - 1) / R;              // row blocks per image
+  const int nb = j1 > j0 ? (j1 - j0) * nrb : 0;  // row blocks of this workgroup
+  const int nA = (R + 4) * PW * 4, nD = nslot * 4;  // 16-B chunks of the two LDS images
   // taps of this wave: wave, wave + 4, ... (7, 6, 6, 6); bias (ones A fragment) on wave 3 of kh 0
   constexpr int MT = 7;
   f32x16 acc[MT], accb;
@@ -175,47 +180,74 @@ __global__ __launch_bounds__(256, 2) void conv2_wgrad_mfma_kernel(const unsigned
   bf16x8 ones;
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
-  for (int j = j0; j < j1; ++j) {
+  // the next row block's operand rows are loaded into registers while the current one computes
+  int4 ra[NA], rd[4];
+  auto fetch = [&](int b) {
+    const int j = j0 + b / nrb, r0 = (b % nrb) * R;
     const int f = j < B2 ? j : j - B2 / 2;
-    for (int r0 = 0; r0 < S1; r0 += R) {
-      const int rows = min(R, S1 - r0);
-      const int npx = rows * S1;
-      __syncthreads();
-      for (int i = tid; i < (R + 4) * PW * 4; i += 256) {   // 16-B chunks, 4 per 32-channel row
+    const int npx = min(R, S1 - r0) * S1;
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+      const int i = tid + 256 * u;
+      ra[u] = make_int4(0, 0, 0, 0);
+      if (i < nA) {
         const int px = i >> 2, c = i & 3;
         const int y = r0 - 2 + px / PW, x = px % PW - 2;
-        int4 v = make_int4(0, 0, 0, 0);
         if (y >= 0 && y < S1 && x >= 0 && x < S1)
-          v = *reinterpret_cast<const int4*>(inb + ((size_t)f * np1 + y * S1 + x) * CH + 32 * kh + 8 * c);
-        *reinterpret_cast<int4*>(ap + px * 32 + 8 * c) = v;
-      }
-      for (int i = tid; i < nslot * 4; i += 256) {
-        const int p = i >> 2, c = i & 3;
-        int4 v = make_int4(0, 0, 0, 0);
-        if (p < npx) v = *reinterpret_cast<const int4*>(db + ((size_t)j * np1 + (size_t)r0 * S1 + p) * CH + 32 * nh + 8 * c);
-        *reinterpret_cast<int4*>(dp + p * 32 + 8 * c) = v;
-      }
-      __syncthreads();
-      for (int s = 0; s < nslot / 16; ++s) {
-        const int klo = 16 * s + 8 * h + q, khi = klo + 4;
-        const int plo = klo < npx ? klo : 0, phi = khi < npx ? khi : 0;
-        const int alo = (plo / S1) * PW + plo % S1, ahi = (phi / S1) * PW + phi % S1;
-        const s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(dp + klo * 32 + col));
-        const s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(dp + khi * 32 + col));
-        const bf16x8 fb = __builtin_bit_cast(bf16x8, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
-#pragma unroll
-        for (int i = 0; i < MT; ++i) {
-          const int t = wave + 4 * i;
-          if (t >= NT) break;
-          const int toff = (t / 5) * PW + t % 5;
-          const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ap + (alo + toff) * 32 + col));
-          const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ap + (ahi + toff) * 32 + col));
-          const bf16x8 fa = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-          acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[i], 0, 0, 0);
-        }
-        if (dobias) accb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb, accb, 0, 0, 0);
+          ra[u] = *reinterpret_cast<const int4*>(inb + ((size_t)f * np1 + y * S1 + x) * CH + 32 * kh + 8 * c);
       }
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = tid + 256 * u;
+      rd[u] = make_int4(0, 0, 0, 0);
+      if (i < nD && (i >> 2) < npx)
+        rd[u] = *reinterpret_cast<const int4*>(db + ((size_t)j * np1 + (size_t)r0 * S1 + (i >> 2)) * CH + 32 * nh + 8 * (i & 3));
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+      const int i = tid + 256 * u;
+      if (i < nA) *reinterpret_cast<int4*>(ap + (i >> 2) * 32 + 8 * (i & 3)) = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = tid + 256 * u;
+      if (i < nD) *reinterpret_cast<int4*>(dp + (i >> 2) * 32 + 8 * (i & 3)) = rd[u];
+    }
+  };
+  if (nb > 0) {
+    fetch(0);
+    commit();
+  }
+  __syncthreads();
+  for (int b = 0; b < nb; ++b) {
+    const int r0 = (b % nrb) * R;
+    const int npx = min(R, S1 - r0) * S1;
+    if (b + 1 < nb) fetch(b + 1);
+    for (int s = 0; s < nslot / 16; ++s) {
+      const int klo = 16 * s + 8 * h + q, khi = klo + 4;
+      const int plo = klo < npx ? klo : 0, phi = khi < npx ? khi : 0;
+      const int alo = (plo / S1) * PW + plo % S1, ahi = (phi / S1) * PW + phi % S1;
+      const s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(dp + klo * 32 + col));
+      const s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(dp + khi * 32 + col));
+      const bf16x8 fb = __builtin_bit_cast(bf16x8, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int t = wave + 4 * i;
+        if (t >= NT) break;
+        const int toff = (t / 5) * PW + t % 5;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ap + (alo + toff) * 32 + col));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ap + (ahi + toff) * 32 + col));
+        const bf16x8 fa = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[i], 0, 0, 0);
+      }
+      if (dobias) accb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb, accb, 0, 0, 0);
+    }
+    __syncthreads();
+    if (b + 1 < nb) commit();
+    __syncthreads();
   }
   float* out = slab + ((size_t)grp * nchunk + chunk) * (NT * CH + 1) * CH;
   const int n = 32 * nh + (lane & 31);
@@ -287,8 +319,16 @@ hipError_t launch_conv2_wgrad_mfma(const ConvTower& T, int B, hipStream_t st) {
   const int B2 = 2 * B;
   const int nchunk = T.nchunk2m, ipc = (B2 + nchunk - 1) / nchunk;
   const int groups8 = (2 * nchunk + 7) / 8;
-  hipLaunchKernelGGL(conv2_wgrad_mfma_kernel, dim3(groups8 * 32), dim3(256), conv2_wgrad_lds(T.S1), st,
-                     T.n1b, T.da2b, T.S1, conv2_wgrad_rows(T.S1), B2, nchunk, ipc, T.slab);
+  const int R = conv2_wgrad_rows(T.S1);
+  const int chunks = (R + 4) * (T.S1 + 4) * 4;   // 16-B chunks of the A image per thread block
+  if (chunks <= 8 * 256)
+    hipLaunchKernelGGL(conv2_wgrad_mfma_kernel<8>, dim3(groups8 * 32), dim3(256), conv2_wgrad_lds(T.S1), st,
+                       T.n1b, T.da2b, T.S1, R, B2, nchunk, ipc, T.slab);
+  else if (chunks <= 16 * 256)
+    hipLaunchKernelGGL(conv2_wgrad_mfma_kernel<16>, dim3(groups8 * 32), dim3(256), conv2_wgrad_lds(T.S1), st,
+                       T.n1b, T.da2b, T.S1, R, B2, nchunk, ipc, T.slab);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -43,15 +43,20 @@ __device__ __forceinline__ float win_sum(float v, int c) {
   return s;
 }
 
+// s^-beta for s >= 1 (the LRN scale: bias 1): native v_log_f32 / v_exp_f32
+__device__ __forceinline__ float pow_nbeta(float s) {
+  return __builtin_amdgcn_exp2f(-LRN_BETA * __builtin_amdgcn_logf(s));
+}
+
 __device__ __forceinline__ float lrn_fwd(float a, int c) {
   const float s = LRN_BIAS + LRN_ALPHA * win_sum(a * a, c);
-  return a * powf(s, -LRN_BETA);
+  return a * pow_nbeta(s);
 }
 
 // d a_c of out = lrn(a) given d out (g), TF LRNGrad
 __device__ __forceinline__ float lrn_bwd(float a, float g, int c) {
   const float s = LRN_BIAS + LRN_ALPHA * win_sum(a * a, c);
-  const float sb = powf(s, -LRN_BETA);
+  const float sb = pow_nbeta(s);
   const float inner = win_sum(g * a * sb / s, c);
   return g * sb - 2.f * LRN_ALPHA * LRN_BETA * a * inner;
 }
@@ -71,54 +76,61 @@ __device__ __forceinline__ void put_planes(unsigned short* p, long long ps, int 
 }
 
 // ---------------------------------------------------------------- conv1 + pool1 + LRN1
-// One wave per pooled pixel, lane = output channel. The 6x6 input patch of the 2x2 window
-// is loaded once per lane (same addresses across the wave: broadcast), the four conv outputs
-// are formed in registers, ReLU, first-max pooling, then LRN across the lanes.
-// w: conv1 block [26][64] (25 taps, bias row). Writes p1 (pooled, for LRN1's backward), arg1
-// (window position of the max), n1 (conv2's input) and, when n1b, its bf16 image.
+// Workgroup: one image, one pooled row qy, a segment of SEG pooled columns. The segment's
+// 6 x (2*SEG + 4) input patch is staged in LDS once; each wave then takes pooled pixels
+// w, w+4, ... with lane = output channel, reading the 36 patch values it needs as LDS
+// broadcasts. The four conv outputs of the 2x2 window are formed in registers, ReLU,
+// first-max pooling, then LRN across the lanes. w: conv1 block [26][64] (25 taps, bias row).
+// Writes p1 (pooled, for LRN1's backward), arg1 (window position of the max), n1 (conv2's
+// input) and, when n1b, its bf16 image.
+constexpr int SEG_MAX = 32;
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict__ xs, int ldx,
-                                                        const float* __restrict__ w, int S, int nimg,
+                                                        const float* __restrict__ w, int S, int seg,
                                                         float* __restrict__ p1, unsigned char* __restrict__ arg1,
                                                         float* __restrict__ n1, unsigned short* __restrict__ n1b) {
-  const int lane = threadIdx.x & 63;
+  __shared__ float patch[6][2 * SEG_MAX + 4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int S1 = S / 2;
-  const long long P = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (P >= (long long)nimg * S1 * S1) return;  // wave-uniform
-  const int img = (int)(P / (S1 * S1));
-  const int pp = (int)(P - (long long)img * S1 * S1);
-  const int py = pp / S1, px = pp - py * S1;
+  const int img = blockIdx.z, qy = blockIdx.y, qx0 = blockIdx.x * seg;
+  const int nq = min(seg, S1 - qx0);
+  const int pw = 2 * nq + 4;
+  const float* x = xs + (size_t)img * ldx;
+  for (int i = threadIdx.x; i < 6 * pw; i += 256) {
+    const int r = i / pw, cc = i % pw;
+    const int y = 2 * qy - 2 + r, xx = 2 * qx0 - 2 + cc;
+    patch[r][cc] = (y >= 0 && y < S && xx >= 0 && xx < S) ? x[y * S + xx] : 0.f;
+  }
   float wr[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) wr[t] = w[t * CH + lane];
   const float b = w[NT * CH + lane];
-  const float* x = xs + (size_t)img * ldx;
-  float patch[36];
+  __syncthreads();
+  for (int q = wv; q < nq; q += 4) {
+    float pv[36];
 #pragma unroll
-  for (int i = 0; i < 6; ++i)
+    for (int i = 0; i < 6; ++i)
 #pragma unroll
-    for (int j = 0; j < 6; ++j) {
-      const int y = 2 * py - 2 + i, xx = 2 * px - 2 + j;
-      patch[i * 6 + j] = (y >= 0 && y < S && xx >= 0 && xx < S) ? x[y * S + xx] : 0.f;
+      for (int j = 0; j < 6; ++j) pv[i * 6 + j] = patch[i][2 * q + j];
+    float best = -INFINITY;
+    int arg = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int dy = k >> 1, dx = k & 1;
+      float acc = b;
+#pragma unroll
+      for (int ky = 0; ky < KS; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < KS; ++kx) acc = fmaf(pv[(dy + ky) * 6 + dx + kx], wr[ky * KS + kx], acc);
+      const float v = fmaxf(acc, 0.f);
+      if (v > best) { best = v; arg = k; }
     }
-  float best = -INFINITY;
-  int arg = 0;
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int dy = q >> 1, dx = q & 1;
-    float acc = b;
-#pragma unroll
-    for (int ky = 0; ky < KS; ++ky)
-#pragma unroll
-      for (int kx = 0; kx < KS; ++kx) acc = fmaf(patch[(dy + ky) * 6 + dx + kx], wr[ky * KS + kx], acc);
-    const float v = fmaxf(acc, 0.f);
-    if (v > best) { best = v; arg = q; }
+    const size_t o = (((size_t)img * S1 + qy) * S1 + qx0 + q) * CH + lane;
+    p1[o] = best;
+    arg1[o] = (unsigned char)arg;
+    const float nv = lrn_fwd(best, lane);
+    if (n1) n1[o] = nv;
+    if (n1b) n1b[o] = bf16_bits(nv);
   }
-  const size_t o = (size_t)P * CH + lane;
-  p1[o] = best;
-  arg1[o] = (unsigned char)arg;
-  const float nv = lrn_fwd(best, lane);
-  n1[o] = nv;
-  if (n1b) n1b[o] = bf16_bits(nv);
 }
 
 // ---------------------------------------------------------------- conv2 (fp32 VALU)
@@ -244,72 +256,110 @@ __global__ __launch_bounds__(256) void pool2_bwd_kernel(const float* __restrict_
     if (__ballot(dn != 0.f)) d = lrn_bwd(a, dn, lane);
     d = a > 0.f ? d : 0.f;
     const size_t o = ((size_t)j * S1 * S1 + pix) * CH + lane;
-    da2[o] = d;
+    if (da2) da2[o] = d;
     if (da2b) da2b[o] = bf16_bits(d);
   }
 }
 
-// ---------------------------------------------------------------- LRN1 backward (in place)
-// d[j][p][c] <- LRNGrad(p1[fwd row][p], d) * (p1 > 0): the gradient at the pooled conv1
-// output; the ReLU mask of the window's argmax pixel is (its pooled value > 0).
-__global__ __launch_bounds__(256) void lrn1_bwd_kernel(float* __restrict__ d, const float* __restrict__ p1,
-                                                       int S1, int nimg, int B2) {
-  const int lane = threadIdx.x & 63;
-  const long long P = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (P >= (long long)nimg * S1 * S1) return;
-  const int j = (int)(P / (S1 * S1));
-  const int pp = (int)(P - (long long)j * S1 * S1);
-  const int f = remap(j, B2);
-  const float a = p1[((size_t)f * S1 * S1 + pp) * CH + lane];
-  const size_t o = (size_t)P * CH + lane;
-  const float g = d[o];
-  float r = 0.f;
-  if (__ballot(g != 0.f)) r = lrn_bwd(a, g, lane);
-  d[o] = a > 0.f ? r : 0.f;
-}
-
 // ---------------------------------------------------------------- conv1 weight gradient
-// slab[grp][chunk][t][c] = sum over the chunk's backward images j (group grp: rows
-// [grp*2B, grp*2B + 2B)) and pooled pixels of d1[j][P][c] * x[fwd row][argmax pixel + tap t],
-// t = 25: the bias row. Wave per pooled pixel; the 6x6 input patch lives in lanes 0..35 and
-// each lane gathers its 25 taps by shuffles (its argmax differs per channel).
-__global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restrict__ d1,
+// dn1 = d(LRN-1 output) -> LRNGrad with p1 -> ReLU mask (p1 > 0) = d1, the gradient at the
+// argmax pixel's conv1 pre-activation; slab[grp][chunk][t][c] = sum over the chunk's backward
+// images j (group grp: rows [grp*2B, grp*2B + 2B)) and pooled pixels of
+// d1[j][P][c] * x[fwd row][argmax pixel + tap t], t = 25: the bias row.
+// The workgroup walks the chunk's segments (image, pooled row, QS pooled columns): a segment's
+// dn1 / p1 / arg1 rows and its 6-row input band are staged in LDS, and the NEXT segment's are
+// already loading into registers while this one computes (the walk is otherwise a chain of
+// dependent global loads). Compute: each wave takes pooled columns w, w+4, ... with
+// lane = channel (LRNGrad across the lanes) and gathers its 25 taps from the band at its own
+// argmax offset.
+constexpr int QS = 32;
+__global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restrict__ dn1,
+                                                          const float* __restrict__ p1,
                                                           const unsigned char* __restrict__ arg1,
                                                           const float* __restrict__ xs, int ldx, int S,
                                                           int B2, int ipc, float* __restrict__ slab) {
+  constexpr int BW = 2 * QS + 4;
+  __shared__ float band[6 * BW];
+  __shared__ float sg[QS * CH], sa[QS * CH];
+  __shared__ __attribute__((aligned(8))) unsigned char sr[QS * CH];
   __shared__ float red[4][NT + 1][CH];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int S1 = S / 2, np1 = S1 * S1;
   const int grp = blockIdx.y, chunk = blockIdx.x;
   const int j0 = grp * B2 + chunk * ipc;
   const int j1 = min(j0 + ipc, grp * B2 + B2);
-  float acc[NT + 1] = {};
-  const long long n = (long long)(j1 - j0) * np1;
-  for (long long idx = wv; idx < n; idx += 4) {
-    const int j = j0 + (int)(idx / np1);
-    const int pp = (int)(idx % np1);
+  const int nseg = (S1 + QS - 1) / QS;
+  const int nit = j1 > j0 ? (j1 - j0) * S1 * nseg : 0;
+  float rg[8], ra[8], rb[2];
+  uint2 rr = make_uint2(0, 0);
+  int cur_nq = 0;
+  auto fetch = [&](int it) {
+    const int j = j0 + it / (S1 * nseg);
+    const int rem = it % (S1 * nseg);
+    const int qy = rem / nseg, q0 = (rem % nseg) * QS;
+    const int nq = min(QS, S1 - q0);
     const int f = remap(j, B2);
-    const int py = pp / S1, px = pp - py * S1;
-    float xv = 0.f;
-    if (lane < 36) {
-      const int y = 2 * py - 2 + lane / 6, x = 2 * px - 2 + lane % 6;
-      if (y >= 0 && y < S && x >= 0 && x < S) xv = xs[(size_t)f * ldx + y * S + x];
+    const size_t pg = (size_t)j * np1 + (size_t)qy * S1 + q0;   // first pooled pixel (backward image)
+    const size_t pf = (size_t)f * np1 + (size_t)qy * S1 + q0;   // ... (forward image)
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int e = tid + 256 * u, px = e >> 6;
+      rg[u] = px < nq ? dn1[pg * CH + e] : 0.f;
+      ra[u] = px < nq ? p1[pf * CH + e] : 0.f;
     }
-    const size_t o = ((size_t)j * np1 + pp) * CH + lane;
-    const float v = d1[o];
-    const int ar = arg1[((size_t)f * np1 + pp) * CH + lane];
-    const int base = (ar >> 1) * 6 + (ar & 1);
+    rr = (tid * 8) / CH < nq ? *reinterpret_cast<const uint2*>(arg1 + pf * CH + tid * 8) : make_uint2(0, 0);
+    const float* x = xs + (size_t)f * ldx;
 #pragma unroll
-    for (int ky = 0; ky < KS; ++ky)
+    for (int u = 0; u < 2; ++u) {
+      const int i = tid + 256 * u, r = i / BW, cc = i % BW;
+      const int y = 2 * qy - 2 + r, xx = 2 * q0 - 2 + cc;
+      rb[u] = (i < 6 * BW && y >= 0 && y < S && xx >= 0 && xx < S) ? x[y * S + xx] : 0.f;
+    }
+    return nq;
+  };
+  auto commit = [&]() {
 #pragma unroll
-      for (int kx = 0; kx < KS; ++kx)
-        acc[ky * KS + kx] = fmaf(v, __shfl(xv, base + ky * 6 + kx), acc[ky * KS + kx]);
-    acc[NT] += v;
+    for (int u = 0; u < 8; ++u) { sg[tid + 256 * u] = rg[u]; sa[tid + 256 * u] = ra[u]; }
+    *reinterpret_cast<uint2*>(sr + tid * 8) = rr;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      if (tid + 256 * u < 6 * BW) band[tid + 256 * u] = rb[u];
+  };
+  float acc[NT + 1] = {};
+  if (nit > 0) {
+    cur_nq = fetch(0);
+    commit();
+  }
+  __syncthreads();
+  for (int it = 0; it < nit; ++it) {
+    const int nq = cur_nq;
+    int next_nq = 0;
+    if (it + 1 < nit) next_nq = fetch(it + 1);
+    for (int q = wv; q < nq; q += 4) {
+      const float g = sg[q * CH + lane], a = sa[q * CH + lane];
+      const int ar = sr[q * CH + lane];
+      float v = 0.f;
+      if (__ballot(g != 0.f)) v = lrn_bwd(a, g, lane);
+      v = a > 0.f ? v : 0.f;
+      const float* bp = band + (ar >> 1) * BW + 2 * q + (ar & 1);
+#pragma unroll
+      for (int ky = 0; ky < KS; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < KS; ++kx)
+          acc[ky * KS + kx] = fmaf(v, bp[ky * BW + kx], acc[ky * KS + kx]);
+      acc[NT] += v;
+    }
+    __syncthreads();
+    if (it + 1 < nit) {
+      commit();
+      cur_nq = next_nq;
+    }
+    __syncthreads();
   }
 #pragma unroll
   for (int t = 0; t <= NT; ++t) red[wv][t][lane] = acc[t];
   __syncthreads();
-  for (int i = threadIdx.x; i < (NT + 1) * CH; i += 256) {
+  for (int i = tid; i < (NT + 1) * CH; i += 256) {
     const int t = i / CH, c = i % CH;
     slab[((size_t)grp * gridDim.x + chunk) * (NT + 1) * CH + i] =
         ((red[0][t][c] + red[1][t][c]) + red[2][t][c]) + red[3][t][c];
@@ -397,8 +447,9 @@ __global__ void sum_slabs_kernel(const float* __restrict__ slab, int nchunk, siz
 // ------------------------------------------------------------------ launchers
 hipError_t launch_conv1_fwd(const ConvTower& T, const float* xs, int ldx, const float* w1, int nimg,
                             hipStream_t st) {
-  const size_t waves = (size_t)nimg * T.S1 * T.S1;
-  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(nblk(waves, 4)), dim3(256), 0, st, xs, ldx, w1, T.S, nimg,
+  const int nseg = (T.S1 + SEG_MAX - 1) / SEG_MAX;
+  const int seg = (T.S1 + nseg - 1) / nseg;
+  hipLaunchKernelGGL(conv1_fwd_kernel, dim3(nseg, T.S1, nimg), dim3(256), 0, st, xs, ldx, w1, T.S, seg,
                      T.p1, T.arg1, T.n1, T.n1b);
   return hipGetLastError();
 }
@@ -429,19 +480,12 @@ hipError_t launch_pool2_bwd(const ConvTower& T, const float* dxf, int ldf, int B
   return hipGetLastError();
 }
 
-hipError_t launch_lrn1_bwd(const ConvTower& T, int B, hipStream_t st) {
-  const size_t waves = (size_t)4 * B * T.S1 * T.S1;
-  hipLaunchKernelGGL(lrn1_bwd_kernel, dim3(nblk(waves, 4)), dim3(256), 0, st, T.dn1, T.p1, T.S1, 4 * B,
-                     2 * B);
-  return hipGetLastError();
-}
-
 hipError_t launch_conv1_wgrad(const ConvTower& T, const float* xs, int ldx, int B, float* g1, float* g2,
                               hipStream_t st) {
   const int B2 = 2 * B;
   const int nchunk = T.nchunk1, ipc = (B2 + nchunk - 1) / nchunk;
-  hipLaunchKernelGGL(conv1_wgrad_kernel, dim3(nchunk, 2), dim3(256), 0, st, T.dn1, T.arg1, xs, ldx, T.S,
-                     B2, ipc, T.slab);
+  hipLaunchKernelGGL(conv1_wgrad_kernel, dim3(nchunk, 2), dim3(256), 0, st, T.dn1, T.p1, T.arg1, xs, ldx,
+                     T.S, B2, ipc, T.slab);
   const size_t n = (size_t)(NT + 1) * CH;
   hipLaunchKernelGGL(sum_slabs_kernel, dim3(nblk(n, 256), 2), dim3(256), 0, st, T.slab, nchunk, n, g1, g2);
   return hipGetLastError();

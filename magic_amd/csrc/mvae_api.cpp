@@ -314,7 +314,7 @@ static void build_schedule(mvae_ctx* c) {
     region(c, nm);
   if (c->conv)
     for (const char* nm : {"conv1_fwd", "conv2_fwd", "lrn2_pool2_fwd", "pool2_bwd", "conv2_wgrad",
-                           "conv2_dgrad", "lrn1_bwd", "conv1_wgrad"})
+                           "conv2_dgrad", "conv1_wgrad"})
       region(c, nm);
 }
 
@@ -476,9 +476,9 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     ALLOC(c->xf, 3 * B * c->ldf);
     ALLOC(c->dxf, 4 * B * c->ldf);
     ALLOC(T.p1, 3 * B * a1);
-    ALLOC(T.n1, 3 * B * a1);
+    if (!T.mfma) ALLOC(T.n1, 3 * B * a1);   // the MFMA kernels read the bf16 images only
     ALLOC(T.a2, 3 * B * a1);
-    ALLOC(T.da2, 4 * B * a1);
+    if (!T.mfma) ALLOC(T.da2, 4 * B * a1);
     ALLOC(T.dn1, 4 * B * a1);
     float* tmp = nullptr;
     ALLOC(tmp, (3 * B * a1 + 3) / 4); T.arg1 = reinterpret_cast<unsigned char*>(tmp);
@@ -490,7 +490,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
       ALLOC(tmp, 25 * 64 * 64 / 2); T.w2d = reinterpret_cast<unsigned short*>(tmp);
     }
     const int B2 = 2 * (int)B;
-    T.nchunk1 = std::min(B2, 256);
+    T.nchunk1 = std::min(B2, 1024);
     T.nchunk2 = std::min(B2, 32);
     T.nchunk2m = std::min(B2, 128);
     const size_t s1 = (size_t)2 * T.nchunk1 * 26 * 64;
@@ -997,10 +997,6 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
       {
         TIMED("conv2_dgrad");
         MV_CHECK(launch_conv2(T, false, T.da2, T.da2b, c->theta + c->cv2.off, T.w2d, T.dn1, 4 * c->B, st));
-      }
-      {
-        TIMED("lrn1_bwd");
-        MV_CHECK(launch_lrn1_bwd(T, c->B, st));
       }
       {
         TIMED("conv1_wgrad");

@@ -137,13 +137,13 @@ struct ConvTower {
   int S = 0, S1 = 0, S2 = 0;
   float* p1 = nullptr;             // pool-1 output        [3B][S1*S1][64]
   unsigned char* arg1 = nullptr;   // its window argmax    [3B][S1*S1][64]
-  float* n1 = nullptr;             // LRN-1 output = conv2 input
+  float* n1 = nullptr;             // LRN-1 output = conv2 input (fp32 kernels only)
   unsigned short* n1b = nullptr;   // ... bf16 (MFMA mode)
   float* a2 = nullptr;             // conv2 + ReLU output  [3B][S1*S1][64]
   unsigned char* arg2 = nullptr;   // pool-2 window argmax [3B][S2*S2][64]
-  float* da2 = nullptr;            // d conv2 pre-activation [4B][S1*S1][64]
+  float* da2 = nullptr;            // d conv2 pre-activation [4B][S1*S1][64] (fp32 kernels only)
   unsigned short* da2b = nullptr;  // ... bf16 (MFMA mode)
-  float* dn1 = nullptr;            // d LRN-1 output, then (in place) d conv1 pooled pre-activation
+  float* dn1 = nullptr;            // d LRN-1 output (conv2 data gradient)
   unsigned short *w2f = nullptr, *w2d = nullptr;  // bf16 conv2 kernel images [25][64 n][64 k]
   float* slab = nullptr;           // weight-gradient partial sums (fixed-order reduction)
   int nchunk1 = 1, nchunk2 = 1, nchunk2m = 1;
@@ -157,7 +157,6 @@ hipError_t launch_conv2(const ConvTower& T, bool fwd, const float* in, const uns
 hipError_t launch_lrn2_pool2_fwd(const ConvTower& T, int nimg, float* xf, int ldf, int f32,
                                  const Planes& xfp, hipStream_t st);
 hipError_t launch_pool2_bwd(const ConvTower& T, const float* dxf, int ldf, int B, hipStream_t st);
-hipError_t launch_lrn1_bwd(const ConvTower& T, int B, hipStream_t st);
 hipError_t launch_conv1_wgrad(const ConvTower& T, const float* xs, int ldx, int B, float* g1, float* g2,
                               hipStream_t st);
 hipError_t launch_conv2_wgrad(const ConvTower& T, int B, float* g1, float* g2, hipStream_t st);

@@ -50,13 +50,13 @@ def test_conv_step_f32x():
 def test_conv_step_bf16_mfma(S, B):
     """conv2 forward / data gradient / weight gradient on the bf16 MFMA kernels (each kernel is
     exact to 2e-6 given bf16-rounded operands: test_conv2_kernel). The metric gradient of the
-    conv2 kernel sums lock and key contributions of opposite sign (squared difference), so
-    at a few tiny images its bf16 error relative to the cancelled value reaches ~0.1: held to
-    0.15 there, the documented 5e-2 everywhere else."""
+    conv2 layer sums lock and key contributions of opposite sign (squared difference), so
+    at a few tiny images its bf16 error relative to the cancelled value reaches ~0.1: its W
+    and b are held to 0.15 there, everything else to the documented 5e-2."""
     cfg = tiny_conv("tanh", "sqdiff", True, 10.0, image_size=S, batch=B, precision="bf16",
                     enc=(500, 64) if S == 100 else (40, 24))
     check_step(cfg, density=0.3, tol=5e-2, loss_tol=2e-3, dist_tol=2e-2, adam=False,
-               g2_tol={"enc_conv2_W": 0.15} if S < 100 else None)
+               g2_tol={"enc_conv2_W": 0.15, "enc_conv2_b": 0.15} if S < 100 else None)
 
 
 def test_conv_full_image_f32():
