@@ -279,10 +279,16 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restric
                                                           const float* __restrict__ xs, int ldx, int S,
                                                           int B2, int ipc, float* __restrict__ slab) {
   constexpr int BW = 2 * QS + 4;
-  __shared__ float band[6 * BW];
-  __shared__ float sg[QS * CH], sa[QS * CH];
-  __shared__ __attribute__((aligned(8))) unsigned char sr[QS * CH];
-  __shared__ float red[4][NT + 1][CH];
+  // staging images; the final cross-wave reduction reuses the same LDS (20 KB per workgroup:
+  // several workgroups per CU keep enough segment loads in flight)
+  constexpr int NSTAGE = 6 * BW + 2 * QS * CH + QS * CH / 4;
+  constexpr int NRED = 4 * 13 * CH;   // the 26 accumulator rows reduce in two halves of 13
+  __shared__ __attribute__((aligned(16))) float lds[NSTAGE > NRED ? NSTAGE : NRED];
+  float* band = lds;
+  float* sg = band + 6 * BW;
+  float* sa = sg + QS * CH;
+  unsigned char* sr = reinterpret_cast<unsigned char*>(sa + QS * CH);
+  auto red = reinterpret_cast<float (*)[13][CH]>(lds);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int S1 = S / 2, np1 = S1 * S1;
   const int grp = blockIdx.y, chunk = blockIdx.x;
@@ -356,13 +362,18 @@ __global__ __launch_bounds__(256) void conv1_wgrad_kernel(const float* __restric
     }
     __syncthreads();
   }
+  // staging images dead: the LDS becomes the reduction buffer (two halves of 13 rows)
 #pragma unroll
-  for (int t = 0; t <= NT; ++t) red[wv][t][lane] = acc[t];
-  __syncthreads();
-  for (int i = tid; i < (NT + 1) * CH; i += 256) {
-    const int t = i / CH, c = i % CH;
-    slab[((size_t)grp * gridDim.x + chunk) * (NT + 1) * CH + i] =
-        ((red[0][t][c] + red[1][t][c]) + red[2][t][c]) + red[3][t][c];
+  for (int hf = 0; hf < 2; ++hf) {
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 13; ++t) red[wv][t][lane] = acc[13 * hf + t];
+    __syncthreads();
+    for (int i = tid; i < 13 * CH; i += 256) {
+      const int t = i / CH, c = i % CH;
+      slab[((size_t)grp * gridDim.x + chunk) * (NT + 1) * CH + 13 * hf * CH + i] =
+          ((red[0][t][c] + red[1][t][c]) + red[2][t][c]) + red[3][t][c];
+    }
   }
 }
 
@@ -430,16 +441,29 @@ __global__ __launch_bounds__(256) void conv2_wgrad_valu_kernel(const float* __re
   }
 }
 
-// out_g[i] = sum_{c < nchunk} slab[g][c][i] in chunk order (g = 0: g1 block, g = 1: g2 block)
-__global__ void sum_slabs_kernel(const float* __restrict__ slab, int nchunk, size_t n,
-                                 float* __restrict__ out0, float* __restrict__ out1) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+// out_g[i] = sum_{c < nchunk} slab[g][c][i] (g = 0: g1 block, g = 1: g2 block) in a fixed
+// order: workgroup = 64 consecutive i x 16 chunk lanes; lane r sums chunks r, r+16, ... and the
+// 16 partials are added in lane order (deterministic; many chunks stay parallel)
+__global__ __launch_bounds__(1024) void sum_slabs_kernel(const float* __restrict__ slab, int nchunk,
+                                                         size_t n, float* __restrict__ out0,
+                                                         float* __restrict__ out1) {
+  __shared__ float part[16][64];
+  const int c = threadIdx.x & 63, r = threadIdx.x >> 6;
+  const size_t i = (size_t)blockIdx.x * 64 + c;
   const int g = blockIdx.y;
-  const float* s = slab + (size_t)g * nchunk * n + i;
   float acc = 0.f;
-  for (int c = 0; c < nchunk; ++c) acc += s[(size_t)c * n];
-  (g ? out1 : out0)[i] = acc;
+  if (i < n) {
+    const float* s = slab + (size_t)g * nchunk * n + i;
+    for (int k = r; k < nchunk; k += 16) acc += s[(size_t)k * n];
+  }
+  part[r][c] = acc;
+  __syncthreads();
+  if (r == 0 && i < n) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) t += part[k][c];
+    (g ? out1 : out0)[i] = t;
+  }
 }
 
 }  // namespace
@@ -487,7 +511,7 @@ hipError_t launch_conv1_wgrad(const ConvTower& T, const float* xs, int ldx, int 
   hipLaunchKernelGGL(conv1_wgrad_kernel, dim3(nchunk, 2), dim3(256), 0, st, T.dn1, T.p1, T.arg1, xs, ldx,
                      T.S, B2, ipc, T.slab);
   const size_t n = (size_t)(NT + 1) * CH;
-  hipLaunchKernelGGL(sum_slabs_kernel, dim3(nblk(n, 256), 2), dim3(256), 0, st, T.slab, nchunk, n, g1, g2);
+  hipLaunchKernelGGL(sum_slabs_kernel, dim3(nblk(n, 64), 2), dim3(1024), 0, st, T.slab, nchunk, n, g1, g2);
   return hipGetLastError();
 }
 
@@ -497,13 +521,13 @@ hipError_t launch_conv2_wgrad(const ConvTower& T, int B, float* g1, float* g2, h
   if (T.mfma && T.n1b && T.da2b) {
     hipError_t e = launch_conv2_wgrad_mfma(T, B, st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(sum_slabs_kernel, dim3(nblk(n, 256), 2), dim3(256), 0, st, T.slab, T.nchunk2m, n, g1, g2);
+    hipLaunchKernelGGL(sum_slabs_kernel, dim3(nblk(n, 64), 2), dim3(1024), 0, st, T.slab, T.nchunk2m, n, g1, g2);
     return hipGetLastError();
   }
   const int nchunk = T.nchunk2, ipc = (B2 + nchunk - 1) / nchunk;
   hipLaunchKernelGGL(conv2_wgrad_valu_kernel, dim3(nchunk, 2, NT + 1), dim3(256), 0, st, T.n1, T.da2, T.S1,
                      B2, ipc, T.slab);
-  hipLaunchKernelGGL(sum_slabs_kernel, dim3(nblk(n, 256), 2), dim3(256), 0, st, T.slab, nchunk, n, g1, g2);
+  hipLaunchKernelGGL(sum_slabs_kernel, dim3(nblk(n, 64), 2), dim3(1024), 0, st, T.slab, nchunk, n, g1, g2);
   return hipGetLastError();
 }
 

@@ -15,7 +15,8 @@ class OracleEngine:
         self.cfg = cfg
         self.oc = O.OracleConfig(image_size=cfg.image_size, enc=tuple(cfg.enc), dec=tuple(cfg.dec),
                                  latent=cfg.latent, act=cfg.act, deform_weight=cfg.deform_weight,
-                                 metric=cfg.metric, reciprocal=cfg.reciprocal, lr=tuple(cfg.lr))
+                                 metric=cfg.metric, reciprocal=cfg.reciprocal, lr=tuple(cfg.lr),
+                                 conv=getattr(cfg, "conv", False))
         self.P = {k: np.asarray(v, np.float64) for k, v in P.items()}
         self.st = O.adam_init(self.oc, self.P)
         self.names1 = O.trained_names(self.oc)

@@ -16,13 +16,13 @@ from tests.gpu_helpers import make_inputs, make_params, max_rel
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, metric, q):
+def _worker(rank, world, port, metric, q, conv=False):
     import torch.distributed as dist
     from magic_amd.engine import Engine
     from magic_amd.parallel import DataParallelStep
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    cfg = preset("8c", image_size=24, batch=32, metric=metric)
+    cfg = preset("8c", image_size=24, batch=32, metric=metric, conv=conv)
     B = cfg.batch
     half = B // world
     eng = Engine(cfg.replace(batch=half, global_batch=B), 0)
@@ -38,12 +38,12 @@ def _worker(rank, world, port, metric, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("metric", ["cosine", "sqdiff"])
-def test_dp2_on_gpu_matches_full_batch(metric):
+@pytest.mark.parametrize("metric,conv", [("cosine", False), ("sqdiff", False), ("sqdiff", True)])
+def test_dp2_on_gpu_matches_full_batch(metric, conv):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from magic_amd.engine import Engine
-    cfg = preset("8c", image_size=24, batch=32, metric=metric)
+    cfg = preset("8c", image_size=24, batch=32, metric=metric, conv=conv)
     eng = Engine(cfg, 0)
     eng.load_params(make_params(cfg))
     X, areas, eps = make_inputs(cfg, cfg.batch)
@@ -60,7 +60,7 @@ def test_dp2_on_gpu_matches_full_batch(metric):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, metric, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, metric, q, conv)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((r, (g, l)) for r, g, l in (q.get(timeout=300) for _ in range(2)))

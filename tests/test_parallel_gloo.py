@@ -19,9 +19,9 @@ from oracle import mvae_oracle as O
 from tests.cpu_engine import OracleEngine
 
 
-def _cfg(metric, recip):
+def _cfg(metric, recip, conv=False):
     return MVAEConfig(image_size=8, batch=6, enc=(20, 16), dec=(12, 10), latent=5, act="tanh",
-                      metric=metric, reciprocal=recip, deform_weight=10.0, lr=(1e-3, 1e-4))
+                      metric=metric, reciprocal=recip, deform_weight=10.0, lr=(1e-3, 1e-4), conv=conv)
 
 
 def _inputs(cfg, B):
@@ -32,13 +32,13 @@ def _inputs(cfg, B):
     return torch.from_numpy(X), torch.from_numpy(areas), torch.from_numpy(eps)
 
 
-def _worker(rank, world, port, metric, recip, q, overlap=True):
+def _worker(rank, world, port, metric, recip, q, overlap=True, conv=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    cfg = _cfg(metric, recip)
+    cfg = _cfg(metric, recip, conv)
     full_B = cfg.batch * world
     cfg = cfg.replace(global_batch=full_B)
-    oc = O.OracleConfig(image_size=cfg.image_size, enc=cfg.enc, dec=cfg.dec, latent=cfg.latent)
+    oc = O.OracleConfig(image_size=cfg.image_size, enc=cfg.enc, dec=cfg.dec, latent=cfg.latent, conv=conv)
     P = O.init_params(oc, seed=0, dtype=np.float64)
     X, A, E = _inputs(cfg, full_B)
     eng = OracleEngine(cfg, P)
@@ -58,14 +58,16 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("metric,recip,overlap", [("sqdiff", True, True), ("cosine", False, True),
-                                                  ("cosine", True, True), ("cosine", True, False)])
-def test_dp2_equals_single_process(metric, recip, overlap):
+@pytest.mark.parametrize("metric,recip,overlap,conv", [("sqdiff", True, True, False), ("cosine", False, True, False),
+                                                       ("cosine", True, True, False), ("cosine", True, False, False),
+                                                       ("sqdiff", True, True, True), ("cosine", False, True, True)])
+def test_dp2_equals_single_process(metric, recip, overlap, conv):
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, metric, recip, q, overlap)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, metric, recip, q, overlap, conv))
+             for r in range(world)]
     for p in procs:
         p.start()
     res = dict((r, (P, l)) for r, P, l in (q.get(timeout=240) for _ in range(world)))
@@ -73,11 +75,11 @@ def test_dp2_equals_single_process(metric, recip, overlap):
         p.join(timeout=60)
         assert p.exitcode == 0
     # single process on the full batch
-    cfg = _cfg(metric, recip)
+    cfg = _cfg(metric, recip, conv)
     B = cfg.batch * world
     cfg = cfg.replace(batch=B)
     oc = O.OracleConfig(image_size=cfg.image_size, enc=cfg.enc, dec=cfg.dec, latent=cfg.latent,
-                        metric=metric, reciprocal=recip, lr=cfg.lr)
+                        metric=metric, reciprocal=recip, lr=cfg.lr, conv=conv)
     P = O.init_params(oc, seed=0, dtype=np.float64)
     st = O.adam_init(oc, P)
     X, A, E = _inputs(cfg, B)
