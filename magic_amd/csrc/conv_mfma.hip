@@ -34,25 +34,36 @@ constexpr int CH = 64, NT = 25;
 
 __device__ __forceinline__ int swz(int px) { return (px >> 1) & 7; }
 
-template <bool FWD>
-__global__ __launch_bounds__(256, 2) void conv2_mfma_kernel(const unsigned short* __restrict__ in,
+template <bool FWD, int NW, int TPB>
+__global__ __launch_bounds__(64 * NW) void conv2_mfma_kernel(const unsigned short* __restrict__ in,
                                                             const unsigned short* __restrict__ wimg,
                                                             const float* __restrict__ bias,
                                                             float* __restrict__ out, int S1, int BR) {
   extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
   const int PW = S1 + 4, PR = BR + 4;
   unsigned short* patch = lds;                 // [PR*PW][64], 16-B chunks swizzled
-  unsigned short* wb = lds + PR * PW * CH;     // 2 x [64 n][64 k], swizzled by n
+  unsigned short* wb = lds + PR * PW * CH;     // 2 slots x TPB x [64 n][64 k], swizzled by n
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int img = blockIdx.y;
   const int y0 = blockIdx.x * BR;
   const int rows = min(BR, S1 - y0);
   const int npx = rows * S1;
   const size_t ibase = (size_t)img * S1 * S1 * CH;
-  // a tap's 64x64 slice = 512 16-B chunks, two per thread: chunk q -> n = q/8, k chunk q%8
-  int4 wr0 = *reinterpret_cast<const int4*>(wimg + 8 * tid);
-  int4 wr1 = *reinterpret_cast<const int4*>(wimg + 8 * (tid + 256));
-  for (int i = tid; i < PR * PW * 8; i += 256) {
+  // a tap's 64x64 slice = 512 16-B chunks, 512 / (64 NW) per thread: chunk q -> n = q/8, k chunk q%8.
+  // TPB taps per LDS slot (one barrier per slot); two slots
+  constexpr int NT_ = 64 * NW, WCH = 512 / NT_, NG = (NT + TPB - 1) / TPB;
+  int4 wr[TPB][WCH];
+  auto get_w = [&](int g) {
+#pragma unroll
+    for (int j = 0; j < TPB; ++j)
+#pragma unroll
+      for (int u = 0; u < WCH; ++u) {
+        const int t = g * TPB + j;
+        if (t < NT) wr[j][u] = *reinterpret_cast<const int4*>(wimg + (size_t)t * CH * CH + 8 * (tid + NT_ * u));
+      }
+  };
+  get_w(0);
+  for (int i = tid; i < PR * PW * 8; i += NT_) {
     const int px = i >> 3, c = i & 7;
     const int y = y0 - 2 + px / PW, x = px % PW - 2;
     int4 v = make_int4(0, 0, 0, 0);
@@ -61,18 +72,22 @@ __global__ __launch_bounds__(256, 2) void conv2_mfma_kernel(const unsigned short
     *reinterpret_cast<int4*>(patch + px * CH + 8 * (c ^ swz(px))) = v;
   }
   auto put_w = [&](unsigned short* dst) {
-    const int n0 = tid >> 3, n1 = n0 + 32, c = tid & 7;
-    *reinterpret_cast<int4*>(dst + n0 * CH + 8 * (c ^ swz(n0))) = wr0;
-    *reinterpret_cast<int4*>(dst + n1 * CH + 8 * (c ^ swz(n1))) = wr1;
+#pragma unroll
+    for (int j = 0; j < TPB; ++j)
+#pragma unroll
+      for (int u = 0; u < WCH; ++u) {
+        const int q = tid + NT_ * u, n = q >> 3, c = q & 7;
+        *reinterpret_cast<int4*>(dst + j * CH * CH + n * CH + 8 * (c ^ swz(n))) = wr[j][u];
+      }
   };
   put_w(wb);
   __syncthreads();
   const int nfr = (npx + 31) >> 5;
-  const bool has0 = wave < nfr, has1 = wave + 4 < nfr;  // wave-uniform
+  const bool has0 = wave < nfr, has1 = wave + NW < nfr;  // wave-uniform
   int pb[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    const int pl = (wave + 4 * i) * 32 + (lane & 31);
+    const int pl = (wave + NW * i) * 32 + (lane & 31);
     const int q = pl < npx ? pl : 0;
     pb[i] = (q / S1) * PW + q % S1;
   }
@@ -84,12 +99,13 @@ __global__ __launch_bounds__(256, 2) void conv2_mfma_kernel(const unsigned short
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-  for (int t = 0; t < NT; ++t) {
-    const unsigned short* wc = wb + (t & 1) * CH * CH;
-    if (t + 1 < NT) {
-      wr0 = *reinterpret_cast<const int4*>(wimg + (size_t)(t + 1) * CH * CH + 8 * tid);
-      wr1 = *reinterpret_cast<const int4*>(wimg + (size_t)(t + 1) * CH * CH + 8 * (tid + 256));
-    }
+  for (int g = 0; g < NG; ++g) {
+    if (g + 1 < NG) get_w(g + 1);
+#pragma unroll
+   for (int j = 0; j < TPB; ++j) {
+    const int t = g * TPB + j;
+    if (t >= NT) break;
+    const unsigned short* wc = wb + ((g & 1) * TPB + j) * CH * CH;
     const int toff = (t / 5) * PW + t % 5;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
@@ -114,7 +130,8 @@ __global__ __launch_bounds__(256, 2) void conv2_mfma_kernel(const unsigned short
         acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[1][1], 0, 0, 0);
       }
     }
-    if (t + 1 < NT) put_w(wb + ((t + 1) & 1) * CH * CH);
+   }
+    if (g + 1 < NG) put_w(wb + ((g + 1) & 1) * TPB * CH * CH);
     __syncthreads();
   }
   // C: row (pixel) (r&3) + 8(r>>2) + 4h of the fragment, column (channel) lane&31 + 32 nf
@@ -128,7 +145,7 @@ __global__ __launch_bounds__(256, 2) void conv2_mfma_kernel(const unsigned short
       const float b = FWD ? bias[n] : 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int pl = (wave + 4 * i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int pl = (wave + NW * i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         if (pl >= npx) continue;
         float v = acc[i][nf][r];
         if (FWD) v = fmaxf(v + b, 0.f);
@@ -277,15 +294,17 @@ __global__ void conv2_wprep_kernel(const float* __restrict__ W, unsigned short* 
 
 }  // namespace
 
-int conv2_mfma_band(int S1) {
-  int br = std::max(1, std::min(S1, 256 / S1));
-  while (br > 1 && (size_t)(br + 4) * (S1 + 4) * CH * 2 + 2 * CH * CH * 2 > 160 * 1024) --br;
+// band rows of the forward / data-gradient kernel with nw waves (64 nw pixel slots)
+int conv2_mfma_band(int S1, int nw, int tpb) {
+  const size_t wlds = (size_t)2 * tpb * CH * CH * 2;   // two slots of TPB taps
+  int br = std::max(1, std::min(S1, 64 * nw / S1));
+  while (br > 1 && (size_t)(br + 4) * (S1 + 4) * CH * 2 + wlds > 160 * 1024) --br;
   return br;
 }
 
-size_t conv2_mfma_lds(int S1) {
-  const int br = conv2_mfma_band(S1);
-  return (size_t)(br + 4) * (S1 + 4) * CH * 2 + 2 * CH * CH * 2;
+size_t conv2_mfma_lds(int S1, int nw, int tpb) {
+  const int br = conv2_mfma_band(S1, nw, tpb);
+  return (size_t)(br + 4) * (S1 + 4) * CH * 2 + (size_t)2 * tpb * CH * CH * 2;
 }
 
 int conv2_wgrad_rows(int S1) { return std::max(1, std::min(S1, 256 / S1)); }
@@ -304,14 +323,25 @@ hipError_t launch_conv2_wprep(const ConvTower& T, const float* w2, hipStream_t s
 hipError_t launch_conv2_mfma(const ConvTower& T, bool fwd, const unsigned short* inb,
                              const unsigned short* wimg, const float* w2, float* out, int nimg,
                              hipStream_t st) {
-  const int br = conv2_mfma_band(T.S1);
-  const size_t lds = conv2_mfma_lds(T.S1);
+  const int nw = T.conv2_nw == 8 ? 8 : 4;
+  const int tpb = nw == 8 && T.conv2_tpb == 2 ? 2 : 1;
+  const int br = conv2_mfma_band(T.S1, nw, tpb);
+  const size_t lds = conv2_mfma_lds(T.S1, nw, tpb);
   dim3 g((T.S1 + br - 1) / br, nimg);
   const float* bias = w2 + (size_t)NT * CH * CH;
-  if (fwd)
-    hipLaunchKernelGGL(conv2_mfma_kernel<true>, g, dim3(256), lds, st, inb, wimg, bias, out, T.S1, br);
-  else
-    hipLaunchKernelGGL(conv2_mfma_kernel<false>, g, dim3(256), lds, st, inb, wimg, bias, out, T.S1, br);
+#define CONV2_LAUNCH(NW_, TPB_)                                                                     \
+  do {                                                                                             \
+    if (fwd)                                                                                       \
+      hipLaunchKernelGGL((conv2_mfma_kernel<true, NW_, TPB_>), g, dim3(64 * NW_), lds, st, inb,    \
+                         wimg, bias, out, T.S1, br);                                               \
+    else                                                                                           \
+      hipLaunchKernelGGL((conv2_mfma_kernel<false, NW_, TPB_>), g, dim3(64 * NW_), lds, st, inb,   \
+                         wimg, bias, out, T.S1, br);                                               \
+  } while (0)
+  if (nw == 8 && tpb == 2) CONV2_LAUNCH(8, 2);
+  else if (nw == 8) CONV2_LAUNCH(8, 1);
+  else CONV2_LAUNCH(4, 1);
+#undef CONV2_LAUNCH
   return hipGetLastError();
 }
 
