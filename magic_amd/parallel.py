@@ -30,7 +30,8 @@ class DataParallelStep:
     ``colsq``, ``coldot``, ``grads``, ``losses`` (the HIP ``Engine``; tests also drive a
     CPU stand-in built on the oracle)."""
 
-    def __init__(self, engine, group=None, reduce_losses: bool = True, overlap: bool = True):
+    def __init__(self, engine, group=None, reduce_losses: bool = True, overlap: bool = True,
+                 force_collectives: bool = False):
         self.e = engine
         # bucketed all-reduce overlapped with the rest of the backward (engines exposing
         # backward_part/grad_ranges); otherwise one bucket after the whole backward
@@ -38,6 +39,9 @@ class DataParallelStep:
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.reduce_losses = reduce_losses
+        # force_collectives: issue the collectives even in a one-rank group (tests run the RCCL
+        # path -- async all-reduces of the library's buffers on its streams -- on a 1-GPU box)
+        self.coll = self.world > 1 or (force_collectives and dist.is_initialized())
         self.cosine = engine.cfg.metric == "cosine"
         if engine.cfg.gbatch != engine.cfg.batch * self.world:
             raise ValueError(f"engine global_batch {engine.cfg.gbatch} != batch {engine.cfg.batch} "
@@ -49,7 +53,7 @@ class DataParallelStep:
             engine.set_shard(self.rank * engine.cfg.batch)
 
     def _ar(self, t):
-        if self.world > 1:
+        if self.coll:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
     def step(self, x, areas, eps=None):
@@ -60,7 +64,7 @@ class DataParallelStep:
         e.metric(areas)
         if self.cosine:
             self._ar(e.coldot)
-        if self.world > 1 and self.overlap:
+        if self.coll and self.overlap:
             handles = []
             for part in range(e.N_BACKWARD_PARTS):
                 e.backward_part(part)

@@ -72,3 +72,57 @@ def test_dp2_on_gpu_matches_full_batch(metric, conv):
         np.testing.assert_allclose(l, l_ref, rtol=1e-4)
         assert max_rel(g, g_ref) <= 1e-4
     np.testing.assert_array_equal(res[0][0], res[1][0])
+
+
+def _rccl_worker(port, metric, conv, q):
+    import torch.distributed as dist
+    from magic_amd.engine import Engine
+    from magic_amd.parallel import DataParallelStep
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    cfg = preset("8c", image_size=24, batch=32, metric=metric, conv=conv)
+    eng = Engine(cfg, 0)
+    eng.load_params(make_params(cfg))
+    X, areas, eps = make_inputs(cfg, cfg.batch)
+    st = DataParallelStep(eng, force_collectives=True)
+    assert st.coll
+    for _ in range(2):
+        st.step(torch.from_numpy(X).cuda(), torch.from_numpy(areas).cuda(), torch.from_numpy(eps).cuda())
+    torch.cuda.synchronize()
+    q.put((eng.params()["enc_h0_W"].cpu().numpy(), eng.grads.cpu().numpy(), eng.losses.cpu().numpy()))
+    eng.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("metric,conv", [("cosine", False), ("sqdiff", True)])
+def test_rccl_collective_path_one_rank(metric, conv):
+    """The RCCL code path of DataParallelStep (backend "nccl": async all-reduces of the
+    library-owned gradient ranges while the later backward parts run, colsq/coldot and loss
+    all-reduces) in a one-rank group on this box's GPU: two steps must equal two plain steps
+    bitwise (a one-rank SUM is the identity)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from magic_amd.engine import Engine
+    cfg = preset("8c", image_size=24, batch=32, metric=metric, conv=conv)
+    eng = Engine(cfg, 0)
+    eng.load_params(make_params(cfg))
+    X, areas, eps = make_inputs(cfg, cfg.batch)
+    for _ in range(2):
+        eng.train_step(torch.from_numpy(X).cuda(), torch.from_numpy(areas).cuda(), torch.from_numpy(eps).cuda())
+    torch.cuda.synchronize()
+    w_ref, g_ref = eng.params()["enc_h0_W"].cpu().numpy(), eng.grads.cpu().numpy()
+    eng.close()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(port, metric, conv, q))
+    p.start()
+    w, g, _ = q.get(timeout=300)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    np.testing.assert_array_equal(g, g_ref)
+    np.testing.assert_array_equal(w, w_ref)
