@@ -281,6 +281,148 @@ __global__ __launch_bounds__(256, 2) void conv2_wgrad_mfma_kernel(const unsigned
   if (dobias && h == 0) out[(size_t)NT * CH * CH + n] = accb[0];
 }
 
+// Weight gradient, 8-wave form: a workgroup owns one 32-channel half of k and ALL 64 n for the
+// 25 taps (waves take taps w, w+8, ...: 4,3,...,3 taps x 2 n-halves of accumulators), so one
+// B fragment pair (both n halves) serves every tap of the wave and only the two k halves of a
+// chunk read the same d rows. d rows are 128 B (64 n): 16-B chunks of rows with (p>>1)&1 swap
+// their 64-B halves, so the four rows of a tr16 group hit four distinct 64-B bank groups.
+// Grid: 8 * ceil(2 * nchunk * 2 / 8); id -> (XCD = id & 7, k half = (id >> 3) & 1, chunk group).
+template <int NA>
+__global__ __launch_bounds__(512) void conv2_wgrad_mfma8_kernel(const unsigned short* __restrict__ inb,
+                                                                const unsigned short* __restrict__ db,
+                                                                int S1, int R, int B2, int nchunk, int ipc,
+                                                                float* __restrict__ slab) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  const int PW = S1 + 4;
+  const int nslot = ((R * S1 + 15) / 16) * 16;
+  unsigned short* ap = lds;                      // [(R+4)*PW][32]
+  unsigned short* dp = lds + (R + 4) * PW * 32;  // [nslot][64], 64-B halves swapped by (p>>1)&1
+  const int id = blockIdx.x;
+  const int xcd = id & 7, kh = (id >> 3) & 1, cgi = (id >> 4) * 8 + xcd;
+  if (cgi >= 2 * nchunk) return;                 // workgroup-uniform
+  const int grp = cgi / nchunk, chunk = cgi % nchunk;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j0 = grp * B2 + chunk * ipc;
+  const int j1 = min(j0 + ipc, grp * B2 + B2);
+  const int np1 = S1 * S1;
+  const int nrb = (S1 + R - 1) / R;
+  const int nb = j1 > j0 ? (j1 - j0) * nrb : 0;
+  const int nA = (R + 4) * PW * 4, nD = nslot * 8;
+  constexpr int MT = 4;                          // taps per wave (at most)
+  f32x16 acc[MT][2], accb[2];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int n2 = 0; n2 < 2; ++n2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][n2][r] = 0.f;
+#pragma unroll
+  for (int n2 = 0; n2 < 2; ++n2)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) accb[n2][r] = 0.f;
+  const bool dobias = kh == 0 && wave == 7;      // wave 7 holds 3 taps: room for the bias rows
+  const int i16 = lane & 15, q = i16 >> 2, pq = i16 & 3, h = lane >> 5, g1 = (lane >> 4) & 1;
+  const int col = 16 * g1 + 4 * pq;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
+  int4 ra[NA], rd[4];
+  auto fetch = [&](int b) {
+    const int j = j0 + b / nrb, r0 = (b % nrb) * R;
+    const int f = j < B2 ? j : j - B2 / 2;
+    const int npx = min(R, S1 - r0) * S1;
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+      const int i = tid + 512 * u;
+      ra[u] = make_int4(0, 0, 0, 0);
+      if (i < nA) {
+        const int px = i >> 2, c = i & 3;
+        const int y = r0 - 2 + px / PW, x = px % PW - 2;
+        if (y >= 0 && y < S1 && x >= 0 && x < S1)
+          ra[u] = *reinterpret_cast<const int4*>(inb + ((size_t)f * np1 + y * S1 + x) * CH + 32 * kh + 8 * c);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = tid + 512 * u;
+      rd[u] = make_int4(0, 0, 0, 0);
+      if (i < nD && (i >> 3) < npx)
+        rd[u] = *reinterpret_cast<const int4*>(db + ((size_t)j * np1 + (size_t)r0 * S1 + (i >> 3)) * CH + 8 * (i & 7));
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int u = 0; u < NA; ++u) {
+      const int i = tid + 512 * u;
+      if (i < nA) *reinterpret_cast<int4*>(ap + (i >> 2) * 32 + 8 * (i & 3)) = ra[u];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = tid + 512 * u;
+      const int p = i >> 3, c = (i & 7) ^ (((p >> 1) & 1) << 2);
+      if (i < nD) *reinterpret_cast<int4*>(dp + p * 64 + 8 * c) = rd[u];
+    }
+  };
+  if (nb > 0) {
+    fetch(0);
+    commit();
+  }
+  __syncthreads();
+  for (int b = 0; b < nb; ++b) {
+    const int r0 = (b % nrb) * R;
+    const int npx = min(R, S1 - r0) * S1;
+    if (b + 1 < nb) fetch(b + 1);
+    for (int s = 0; s < nslot / 16; ++s) {
+      const int klo = 16 * s + 8 * h + q, khi = klo + 4;
+      const int plo = klo < npx ? klo : 0, phi = khi < npx ? khi : 0;
+      const int alo = (plo / S1) * PW + plo % S1, ahi = (phi / S1) * PW + phi % S1;
+      bf16x8 fb[2];
+#pragma unroll
+      for (int n2 = 0; n2 < 2; ++n2) {
+        const int clo = (32 * n2 + col) ^ (((klo >> 1) & 1) << 5);
+        const int chi = (32 * n2 + col) ^ (((khi >> 1) & 1) << 5);
+        const s16x4 blo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(dp + klo * 64 + clo));
+        const s16x4 bhi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(dp + khi * 64 + chi));
+        fb[n2] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(blo, bhi, 0, 1, 2, 3, 4, 5, 6, 7));
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const int t = wave + 8 * i;
+        if (t >= NT) break;
+        const int toff = (t / 5) * PW + t % 5;
+        const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ap + (alo + toff) * 32 + col));
+        const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(ap + (ahi + toff) * 32 + col));
+        const bf16x8 fa = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+        acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb[0], acc[i][0], 0, 0, 0);
+        acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb[1], acc[i][1], 0, 0, 0);
+      }
+      if (dobias) {
+        accb[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[0], accb[0], 0, 0, 0);
+        accb[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, fb[1], accb[1], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (b + 1 < nb) commit();
+    __syncthreads();
+  }
+  float* out = slab + ((size_t)grp * nchunk + chunk) * (NT * CH + 1) * CH;
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    const int t = wave + 8 * i;
+    if (t >= NT) break;
+#pragma unroll
+    for (int n2 = 0; n2 < 2; ++n2)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int k = 32 * kh + (r & 3) + 8 * (r >> 2) + 4 * h;
+        out[(size_t)(t * CH + k) * CH + 32 * n2 + (lane & 31)] = acc[i][n2][r];
+      }
+  }
+  if (dobias && h == 0)
+#pragma unroll
+    for (int n2 = 0; n2 < 2; ++n2) out[(size_t)NT * CH * CH + 32 * n2 + (lane & 31)] = accb[n2][0];
+}
+
 // bf16 kernel images of conv2 for the MFMA kernels, [t][n][k] (k contiguous):
 // forward  wf[t][n][k] = W[t*64 + k][n];  data gradient  wd[t][n][k] = W[(24 - t)*64 + n][k]
 __global__ void conv2_wprep_kernel(const float* __restrict__ W, unsigned short* __restrict__ wf,
@@ -351,6 +493,19 @@ hipError_t launch_conv2_wgrad_mfma(const ConvTower& T, int B, hipStream_t st) {
   const int groups8 = (2 * nchunk + 7) / 8;
   const int R = conv2_wgrad_rows(T.S1);
   const int chunks = (R + 4) * (T.S1 + 4) * 4;   // 16-B chunks of the A image per thread block
+  if (T.conv2_wg8 && (size_t)((R * T.S1 + 15) / 16 * 16) * 8 <= 4 * 512) {
+    const int g16 = (2 * nchunk + 7) / 8;
+    const size_t lds = ((size_t)(R + 4) * (T.S1 + 4) * 32 + (size_t)(R * T.S1 + 15) / 16 * 16 * 64) * 2;
+    if (chunks <= 4 * 512)
+      hipLaunchKernelGGL(conv2_wgrad_mfma8_kernel<4>, dim3(g16 * 16), dim3(512), lds, st, T.n1b, T.da2b, T.S1,
+                         R, B2, nchunk, ipc, T.slab);
+    else if (chunks <= 8 * 512)
+      hipLaunchKernelGGL(conv2_wgrad_mfma8_kernel<8>, dim3(g16 * 16), dim3(512), lds, st, T.n1b, T.da2b, T.S1,
+                         R, B2, nchunk, ipc, T.slab);
+    else
+      return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   if (chunks <= 8 * 256)
     hipLaunchKernelGGL(conv2_wgrad_mfma_kernel<8>, dim3(groups8 * 32), dim3(256), conv2_wgrad_lds(T.S1), st,
                        T.n1b, T.da2b, T.S1, R, B2, nchunk, ipc, T.slab);

@@ -150,6 +150,7 @@ struct ConvTower {
   bool mfma = false;               // conv2 on bf16 MFMA (bf16 mode)
   int conv2_nw = 8;                // waves per workgroup of the conv2 forward / data-gradient kernel
   int conv2_tpb = 1;               // ... and taps per weight slot (one barrier per slot)
+  bool conv2_wg8 = true;           // weight gradient: 8-wave all-n workgroups (else 4-wave quarters)
 };
 hipError_t launch_conv1_fwd(const ConvTower& T, const float* xs, int ldx, const float* w1, int nimg,
                             hipStream_t st);
