@@ -162,6 +162,11 @@ int mvae_train_step(mvae_ctx* ctx, const float* x, const float* areas, const flo
 
 /* ---- inference surface ------------------------------------------------------------ */
 int mvae_predict(mvae_ctx* ctx, const float* x, const float* eps, float* dist_out, void* stream);
+/* The same in two phases: a data-parallel host all-reduces MVAE_BUF_COLSQ (cosine metric)
+ * between them, so every rank's distances use the global batch's column norms as the
+ * single-process call on the whole batch does (8c/vae.py:449-450).                        */
+int mvae_predict_encode(mvae_ctx* ctx, const float* x, const float* eps, void* stream);
+int mvae_predict_finish(mvae_ctx* ctx, float* dist_out, void* stream);
 /* transform: the lock image's latent mean only (no eps draw). */
 int mvae_transform(mvae_ctx* ctx, const float* x, float* zmean_out, void* stream);
 int mvae_reconstruct(mvae_ctx* ctx, const float* x, const float* eps, float* y_out, void* stream);

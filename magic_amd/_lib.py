@@ -75,6 +75,8 @@ _SIGS = {
     "mvae_train_step": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                          C.c_void_p], C.c_int),
     "mvae_predict": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
+    "mvae_predict_encode": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
+    "mvae_predict_finish": ([C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mvae_transform": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mvae_reconstruct": ([C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mvae_generate": ([C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p], C.c_int),

@@ -1090,17 +1090,32 @@ extern "C" int mvae_train_step(mvae_ctx* ctx, const float* x, const float* areas
   return mvae_adam(ctx, stream);
 }
 
-extern "C" int mvae_predict(mvae_ctx* ctx, const float* x, const float* eps, float* dist_out, void* stream) {
-  if (!ctx || !x || !dist_out) return MVAE_EINVAL;
-  hipStream_t st = (hipStream_t)stream;
-  int rc = encode(ctx, x, eps, st, ENC_EVAL);
+// get_predictions in two phases (a data-parallel host all-reduces MVAE_BUF_COLSQ between them:
+// the cosine distance normalises over the GLOBAL batch, 8c/vae.py:449-450)
+extern "C" int mvae_predict_encode(mvae_ctx* ctx, const float* x, const float* eps, void* stream) {
+  if (!ctx || !x) return MVAE_EINVAL;
+  int rc = encode(ctx, x, eps, (hipStream_t)stream, ENC_EVAL);
   if (rc) return rc;
+  ctx->phase = 6;
+  return MVAE_OK;
+}
+
+extern "C" int mvae_predict_finish(mvae_ctx* ctx, float* dist_out, void* stream) {
+  if (!ctx || !dist_out) return MVAE_EINVAL;
+  if (ctx->phase != 6) return fail(ctx, MVAE_ESTATE, "mvae_predict_finish before mvae_predict_encode");
+  hipStream_t st = (hipStream_t)stream;
   auto c = ctx;
   MV_CHECK(launch_metric(c->z, c->ldz, c->ms, c->rowpart, c->nblk, nullptr, c->colsq, c->B, c->L,
                          c->cfg.metric, c->cfg.reciprocal, c->cfg.deform_weight, c->inv_bg,
                          c->rowvals, dist_out, c->draw, st));
   ctx->phase = 0;
   return MVAE_OK;
+}
+
+extern "C" int mvae_predict(mvae_ctx* ctx, const float* x, const float* eps, float* dist_out, void* stream) {
+  if (!ctx || !x || !dist_out) return MVAE_EINVAL;
+  int rc = mvae_predict_encode(ctx, x, eps, stream);
+  return rc ? rc : mvae_predict_finish(ctx, dist_out, stream);
 }
 
 extern "C" int mvae_transform(mvae_ctx* ctx, const float* x, float* zmean_out, void* stream) {

@@ -230,6 +230,16 @@ class Engine:
         self._check(self.lib.mvae_predict(self.ctx, self._xin(x), _ptr(eps), _ptr(out), self.stream))
         return out
 
+    def predict_encode(self, x, eps=None):
+        """First phase of ``predict``: encoder + (cosine) the local column sums ``colsq``."""
+        self._check(self.lib.mvae_predict_encode(self.ctx, self._xin(x), _ptr(eps), self.stream))
+
+    def predict_finish(self, out=None):
+        """Second phase: distances with the current ``colsq`` (all-reduced under DP)."""
+        out = out if out is not None else torch.empty(self.cfg.batch, device=self.dev)
+        self._check(self.lib.mvae_predict_finish(self.ctx, _ptr(out), self.stream))
+        return out
+
     def transform(self, x, out=None):
         out = out if out is not None else torch.empty(self.cfg.batch, self.cfg.latent, device=self.dev)
         self._check(self.lib.mvae_transform(self.ctx, self._xin(x), _ptr(out), self.stream))

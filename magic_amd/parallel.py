@@ -82,6 +82,19 @@ class DataParallelStep:
         return e.losses
 
 
+    def predict(self, x, eps=None):
+        """``get_predictions`` on this rank's rows with the global batch's cosine column norms
+        (all-reduced ``colsq`` between the two phases); engines without the phases predict
+        locally."""
+        e = self.e
+        if not hasattr(e, "predict_encode"):
+            return e.predict(x, eps)
+        e.predict_encode(x, eps)
+        if self.cosine:
+            self._ar(e.colsq)
+        return e.predict_finish()
+
+
 def shard_rows(t: torch.Tensor, rank: int, world: int) -> torch.Tensor:
     n = t.shape[0] // world
     return t[rank * n:(rank + 1) * n]

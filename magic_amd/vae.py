@@ -110,6 +110,8 @@ class TangoEncoder(object):
 
     def get_predictions(self, X, overlap_areas=None, eps=None):
         e = None if eps is None else self._dev(eps, (3, self.batch_size, self.latent_dimensions))
+        if self._dp is not None:  # cosine column norms over the global batch
+            return self._dp.predict(self._x(X), e).cpu().numpy()
         return self.engine.predict(self._x(X), e).cpu().numpy()
 
     def transform(self, X, overlap_areas=None):

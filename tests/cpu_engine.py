@@ -71,3 +71,13 @@ class OracleEngine:
             g2[n] = g[o:o + self.P[n].size].reshape(self.P[n].shape)
             o += self.P[n].size
         self.P, self.st = O.adam(self.P, g1, g2, self.st, self.oc)
+
+    # get_predictions in the engine's two phases (colsq all-reduced between them under DP)
+    def predict_encode(self, x, eps=None):
+        self.pc = O.forward(self.P, x.numpy(), eps.numpy(), self.oc)
+        self.colsq.copy_(torch.from_numpy(self.pc["colsq"].reshape(-1)))
+
+    def predict_finish(self):
+        cs = self.colsq.numpy().reshape(2, -1)
+        O.metric(self.pc, np.zeros(self.pc["z_l"].shape[0]), self.oc, self.cfg.gbatch, colsq_global=cs)
+        return torch.from_numpy(self.pc["dist"].copy())

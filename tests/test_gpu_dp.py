@@ -126,3 +126,52 @@ def test_rccl_collective_path_one_rank(metric, conv):
     assert p.exitcode == 0
     np.testing.assert_array_equal(g, g_ref)
     np.testing.assert_array_equal(w, w_ref)
+
+
+def _predict_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from magic_amd.engine import Engine
+    from magic_amd.parallel import DataParallelStep
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    cfg = preset("8c", image_size=24, batch=32, metric="cosine")
+    half = cfg.batch // world
+    eng = Engine(cfg.replace(batch=half, global_batch=cfg.batch), 0)
+    eng.load_params(make_params(cfg))
+    X, areas, eps = make_inputs(cfg, cfg.batch)
+    sl = slice(rank * half, (rank + 1) * half)
+    st = DataParallelStep(eng)
+    pred = st.predict(torch.from_numpy(X[sl]).cuda(), torch.from_numpy(np.ascontiguousarray(eps[:, sl])).cuda())
+    q.put((rank, pred.cpu().numpy()))
+    eng.close()
+    dist.destroy_process_group()
+
+
+def test_dp2_predictions_use_global_cosine_norms():
+    """get_predictions under data parallelism: the cosine distance normalises each latent
+    column over the GLOBAL batch (8c/vae.py:449-450); 2 ranks x half the rows must give the
+    single-process predictions on the whole batch."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from magic_amd.engine import Engine
+    cfg = preset("8c", image_size=24, batch=32, metric="cosine")
+    eng = Engine(cfg, 0)
+    eng.load_params(make_params(cfg))
+    X, areas, eps = make_inputs(cfg, cfg.batch)
+    ref = eng.predict(torch.from_numpy(X).cuda(), torch.from_numpy(eps).cuda()).cpu().numpy()
+    eng.close()
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_predict_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    got = np.concatenate([res[0], res[1]])
+    assert max_rel(got, ref) <= 1e-4, max_rel(got, ref)

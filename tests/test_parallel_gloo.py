@@ -46,7 +46,8 @@ def _worker(rank, world, port, metric, recip, q, overlap=True, conv=False):
     for _ in range(2):
         losses = step.step(shard_rows(X, rank, world), shard_rows(A, rank, world),
                            E[:, rank * cfg.batch:(rank + 1) * cfg.batch].contiguous())
-    q.put((rank, {k: v.copy() for k, v in eng.P.items()}, losses.numpy().copy()))
+    pred = step.predict(shard_rows(X, rank, world), E[:, rank * cfg.batch:(rank + 1) * cfg.batch].contiguous())
+    q.put((rank, {k: v.copy() for k, v in eng.P.items()}, losses.numpy().copy(), pred.numpy().copy()))
     dist.destroy_process_group()
 
 
@@ -70,7 +71,7 @@ def test_dp2_equals_single_process(metric, recip, overlap, conv):
              for r in range(world)]
     for p in procs:
         p.start()
-    res = dict((r, (P, l)) for r, P, l in (q.get(timeout=240) for _ in range(world)))
+    res = dict((r, (P, l, pr)) for r, P, l, pr in (q.get(timeout=240) for _ in range(world)))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -85,8 +86,11 @@ def test_dp2_equals_single_process(metric, recip, overlap, conv):
     X, A, E = _inputs(cfg, B)
     for _ in range(2):
         losses, _, P, st, _ = O.train_step(P, st, X.numpy(), A.numpy(), E.numpy(), oc)
+    # get_predictions after the two steps: global-batch cosine norms on every rank
+    pred_full = O.predictions(P, X.numpy(), E.numpy(), oc)
+    np.testing.assert_allclose(np.concatenate([res[r][2] for r in range(world)]), pred_full, rtol=1e-9)
     for r in range(world):
-        Pr, lr_ = res[r]
+        Pr, lr_, _ = res[r]
         np.testing.assert_allclose(lr_, losses, rtol=1e-10)
         for k in O.trained_names(oc):
             np.testing.assert_allclose(Pr[k], P[k], rtol=1e-9, atol=1e-12, err_msg=k)
