@@ -31,14 +31,24 @@ inline unsigned nblk(size_t n, unsigned b) { return (unsigned)((n + b - 1) / b);
 
 __device__ __forceinline__ int remap(int j, int B2) { return j < B2 ? j : j - B2 / 2; }
 
+// whole-wave lane shifts by one (DPP wave_shr:1 / wave_shl:1, GFX9 family): a VALU move, no
+// LDS traffic; bound_ctrl: the lane shifted in reads 0 (the LRN window's clipping at the ends)
+__device__ __forceinline__ float wave_shr1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xf, 0xf, true));
+}
+__device__ __forceinline__ float wave_shl1(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xf, 0xf, true));
+}
+
 // sum over channels |j - c| <= 4 (clipped at 0 and 63) of v_j; lane c holds v_c
 __device__ __forceinline__ float win_sum(float v, int c) {
-  float s = v;
+  (void)c;
+  float s = v, a = v, b = v;
 #pragma unroll
   for (int d = 1; d <= LRN_R; ++d) {
-    const float up = __shfl(v, (c + d) & 63);
-    const float dn = __shfl(v, (c - d) & 63);
-    s += (c + d < CH ? up : 0.f) + (c - d >= 0 ? dn : 0.f);
+    a = wave_shr1(a);
+    b = wave_shl1(b);
+    s += a + b;
   }
   return s;
 }
