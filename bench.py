@@ -151,8 +151,10 @@ def region_bytes(cfg, name: str) -> float:
         return 3 * BL * 4.0 + 2 * BL * 4.0 + B * 4.0 * 6
     if name == "coldot":
         return 2 * BL * 4.0 + B * 4.0
-    if name == "latent_bwd":    # z (3 blocks), mu/s (3 blocks), eps (3), dz_dec in; dhead (4 rows x 2L) out
-        return BL * (12.0 + 24.0 + 12.0 + 4.0) + 4 * BL * 2 * (4.0 + 2.0 * np_)
+    if name == "latent_bwd":    # z (3 blocks), lock mu/s + rot/key s, eps (3), dz_dec in; dhead (4 rows x 2L) out
+        # (fp32 dhead rows only when a native-fp32 head GEMM reads them: f32 mode, or 2L < 256)
+        d32 = 4.0 if (np_ == 0 or 2 * L < 256) else 0.0
+        return BL * (12.0 + 16.0 + 12.0 + 4.0) + 4 * BL * 2 * (d32 + 2.0 * np_)
     if cfg.conv:  # the conv tower's per-pixel kernels (magic_amd/csrc/conv_tower.hip)
         S1 = cfg.image_size // 2
         A1 = S1 * S1 * 64.0                # elements of one image after pool 1

@@ -72,6 +72,7 @@ struct mvae_ctx {
   std::vector<float*> dzl;  // dZ of every encoder layer [4B][lddz] (all live until its wgrad)
   int enc_part1 = 0;        // bwd_enc[0, enc_part1): dgrad chain + layer-0 wgrad
   float* zgen = nullptr;
+  int dhead32 = 1;           // latent_bwd writes fp32 dhead rows (some fp32 GEMM reads them)
   float* ws = nullptr;       // split-K slabs of GEMMs on the caller's stream
   float* ws_side = nullptr;  // ... and of GEMMs on the side stream (concurrent)
   size_t ws_elems = 0;
@@ -617,6 +618,11 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
       d->epi.c32 = fp32_reader ? 1 : 0;
     }
   }
+  if (c->np) {  // fp32 dhead only for a native-fp32 head GEMM (else its planes alone)
+    c->dhead32 = 0;
+    for (auto& d : c->bwd_enc)
+      if (d.prec == GEMM_F32 && (d.A == c->dhead || d.B == c->dhead)) c->dhead32 = 1;
+  }
   if (c->conv) {
     // conv1 reads the fp32 pixels of all three row blocks (forward and weight gradient); the
     // fp32 feature rows are written only when an fp32 GEMM reads them
@@ -965,7 +971,8 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
     {
       TIMED("latent_bwd");
       MV_CHECK(launch_latent_bwd(c->z, c->ldz, c->ms, c->eps, c->dzdec, c->draw, c->colsq, c->coldot,
-                                 c->B, c->L, c->cfg.metric, c->cfg.deform_weight, c->inv_bg, c->dhead,
+                                 c->B, c->L, c->cfg.metric, c->cfg.deform_weight, c->inv_bg,
+                                 c->dhead32 ? c->dhead : nullptr,
                                  c->ld_dh, planes_of(c, c->dhead), st));
     }
     // bwd_enc: [dgrad(n) .. dgrad(1), wgrad(0) | wgrad(n), wgrad(n-1) .. wgrad(1)]; dgrad(i)

@@ -343,46 +343,53 @@ __global__ void latent_bwd_kernel(const float* __restrict__ z, int ldz, const fl
                                   const float* __restrict__ coldot, int B, int L, int metric,
                                   float w, float inv_bg, float* __restrict__ dhead, int ldh,
                                   unsigned short* __restrict__ hp, long long ps, int np) {
+  // one thread per (b, i): the four backward rows of element i of pair b from one read of its
+  // three z values, the lock mu/s and the rot/key s, the three eps and dz_dec
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (size_t)4 * B * L) return;
-  const int r = (int)(idx / L), i = (int)(idx - (size_t)r * L);
-  const int q = r / B, b = r - q * B;
+  if (idx >= (size_t)B * L) return;
+  const int b = (int)(idx / L), i = (int)(idx - (size_t)b * L);
   const float zr = z[(size_t)b * ldz + i];
   const float zl = z[(size_t)(B + b) * ldz + i];
   const float zk = z[(size_t)(2 * B + b) * ldz + i];
-  const int fwd_blk = q == 0 ? 0 : (q == 3 ? 2 : 1);
-  const int frow = fwd_blk * B + b;
-  const float mu = ms[(size_t)frow * 2 * L + i];
-  const float s = ms[(size_t)frow * 2 * L + L + i];
-  const float e = eps[((size_t)eps_slot(fwd_blk) * B + b) * L + i];
-  const float sig = sqrtf(expf(s));
-  float dz, dmu_extra = 0.f, ds_extra = 0.f;
-  if (q == 0) {
-    dz = -2.f * w * (zl - zr) * inv_bg;
-  } else if (q == 1) {
-    dz = dzdec[(size_t)b * L + i] + 2.f * w * (zl - zr) * inv_bg;
-    dmu_extra = mu * inv_bg;
-    ds_extra = 0.5f * (expf(s) - 1.f) * inv_bg;
-  } else {
+  const float s_r = ms[(size_t)b * 2 * L + L + i];
+  const float mu_l = ms[(size_t)(B + b) * 2 * L + i];
+  const float s_l = ms[(size_t)(B + b) * 2 * L + L + i];
+  const float s_k = ms[(size_t)(2 * B + b) * 2 * L + L + i];
+  const float e_r = eps[((size_t)eps_slot(0) * B + b) * L + i];
+  const float e_l = eps[((size_t)eps_slot(1) * B + b) * L + i];
+  const float e_k = eps[((size_t)eps_slot(2) * B + b) * L + i];
+  const float ex_l = expf(s_l);
+  const float sig_r = sqrtf(expf(s_r)), sig_l = sqrtf(ex_l), sig_k = sqrtf(expf(s_k));
+  const float def = 2.f * w * (zl - zr) * inv_bg;
+  float dz2, dz3;  // g2 rows: lock, key
+  {
     const float dr = draw[b];
     if (metric == 1) {
-      const float d = 2.f * dr * (zl - zk);
-      dz = q == 2 ? d : -d;
+      dz2 = 2.f * dr * (zl - zk);
+      dz3 = -dz2;
     } else {
       const float ssl = colsq[i], ssk = colsq[L + i];
       const float rl = rsqrtf(fmaxf(ssl, L2_EPS)), rk = rsqrtf(fmaxf(ssk, L2_EPS));
       const float nl = zl * rl, nk = zk * rk, c = coldot[i];
-      if (q == 2) dz = rl * (dr * nk - (ssl >= L2_EPS ? nl * c : 0.f));
-      else        dz = rk * (dr * nl - (ssk >= L2_EPS ? nk * c : 0.f));
+      dz2 = rl * (dr * nk - (ssl >= L2_EPS ? nl * c : 0.f));
+      dz3 = rk * (dr * nl - (ssk >= L2_EPS ? nk * c : 0.f));
     }
   }
-  const float dmu = dz + dmu_extra;
-  const float ds = 0.5f * dz * e * sig + ds_extra;
-  dhead[(size_t)r * ldh + i] = dmu;
-  dhead[(size_t)r * ldh + L + i] = ds;
-  if (hp) {
-    planes_put(hp, ps, np, (size_t)r * ldh + i, dmu);
-    planes_put(hp, ps, np, (size_t)r * ldh + L + i, ds);
+  const float dz1 = dzdec[(size_t)b * L + i] + def;
+  const float dmu[4] = {-def, dz1 + mu_l * inv_bg, dz2, dz3};
+  const float ds[4] = {-0.5f * def * e_r * sig_r, 0.5f * dz1 * e_l * sig_l + 0.5f * (ex_l - 1.f) * inv_bg,
+                       0.5f * dz2 * e_l * sig_l, 0.5f * dz3 * e_k * sig_k};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const size_t o = (size_t)(q * B + b) * ldh;
+    if (dhead) {
+      dhead[o + i] = dmu[q];
+      dhead[o + L + i] = ds[q];
+    }
+    if (hp) {
+      planes_put(hp, ps, np, o + i, dmu[q]);
+      planes_put(hp, ps, np, o + L + i, ds[q]);
+    }
   }
 }
 
@@ -531,7 +538,7 @@ hipError_t launch_latent_bwd(const float* z, int ldz, const float* ms, const flo
                              const float* dzdec, const float* draw, const float* colsq,
                              const float* coldot, int B, int L, int metric, float w, float inv_bg,
                              float* dhead, int ldh, const Planes& hp, hipStream_t st) {
-  const size_t n = (size_t)4 * B * L;
+  const size_t n = (size_t)B * L;
   hipLaunchKernelGGL(latent_bwd_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, z, ldz, ms, eps, dzdec,
                      draw, colsq, coldot, B, L, metric, w, inv_bg, dhead, ldh, hp.p, hp.stride, hp.n);
   return hipGetLastError();
