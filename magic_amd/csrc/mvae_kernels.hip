@@ -182,7 +182,8 @@ __global__ void normal_kernel(float* __restrict__ out, int B, int L, int Bg, int
 }
 
 // ---------------------------------------------------------------- reparameterisation
-// z = mu + sqrt(exp(s)) * eps   (11a/vae.py:371-377); ms rows = [mu | s] (2L wide)
+// z = mu + sqrt(exp(s)) * eps   (11a/vae.py:371-377); ms rows = [mu | s] (2L wide). The bf16
+// planes of z are written for the lock block only: the decoder's GEMMs read no other rows.
 __global__ void latent_fwd_kernel(const float* __restrict__ ms, const float* __restrict__ eps,
                                   float* __restrict__ z, unsigned short* __restrict__ zp,
                                   long long ps, int np, int B, int L, int ldz) {
@@ -195,7 +196,31 @@ __global__ void latent_fwd_kernel(const float* __restrict__ ms, const float* __r
   const float e = eps[((size_t)eps_slot(blk) * B + b) * L + i];
   const float v = mu + sqrtf(expf(s)) * e;
   z[(size_t)r * ldz + i] = v;
-  if (zp) planes_put(zp, ps, np, (size_t)r * ldz + i, v);
+  if (zp && blk == 1) planes_put(zp, ps, np, (size_t)r * ldz + i, v);
+}
+
+// the same, 4 consecutive elements per thread (L % 4 == 0: 16-B rows of ms, eps and z)
+__global__ void latent_fwd4_kernel(const float* __restrict__ ms, const float* __restrict__ eps,
+                                   float* __restrict__ z, unsigned short* __restrict__ zp,
+                                   long long ps, int np, int B, int L, int ldz) {
+  const int L4 = L / 4;
+  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (size_t)3 * B * L4) return;
+  const int r = (int)(idx / L4), i = 4 * (int)(idx - (size_t)r * L4);
+  const int blk = r / B, b = r - blk * B;
+  const float4 mu = *reinterpret_cast<const float4*>(ms + (size_t)r * 2 * L + i);
+  const float4 s = *reinterpret_cast<const float4*>(ms + (size_t)r * 2 * L + L + i);
+  const float4 e = *reinterpret_cast<const float4*>(eps + ((size_t)eps_slot(blk) * B + b) * L + i);
+  const float4 v = make_float4(mu.x + sqrtf(expf(s.x)) * e.x, mu.y + sqrtf(expf(s.y)) * e.y,
+                               mu.z + sqrtf(expf(s.z)) * e.z, mu.w + sqrtf(expf(s.w)) * e.w);
+  const size_t o = (size_t)r * ldz + i;
+  *reinterpret_cast<float4*>(z + o) = v;
+  if (zp && blk == 1) {
+    planes_put(zp, ps, np, o, v.x);
+    planes_put(zp, ps, np, o + 1, v.y);
+    planes_put(zp, ps, np, o + 2, v.z);
+    planes_put(zp, ps, np, o + 3, v.w);
+  }
 }
 
 // ---------------------------------------------------------------- column statistics
@@ -265,19 +290,33 @@ __global__ void metric_kernel(const float* __restrict__ z, int ldz, const float*
   const float* zk = z + (size_t)(2 * B + b) * ldz;
   const float* msl = ms + (size_t)(B + b) * 2 * L;
   float kl = 0.f, fd = 0.f, raw = 0.f, rp = 0.f;
-  for (int i = lane; i < L; i += 64) {
-    const float mu = msl[i], s = msl[L + i];
+  auto term = [&](float mu, float s, float l, float r, float k, int i) {
     kl += 1.f + s - mu * mu - expf(s);
-    const float d = zl[i] - zr[i];
+    const float d = l - r;
     fd += d * d;
     if (metric == 0) {
       const float rl = rsqrtf(fmaxf(colsq[i], L2_EPS));
       const float rk = rsqrtf(fmaxf(colsq[L + i], L2_EPS));
-      raw += (zl[i] * rl) * (zk[i] * rk);
+      raw += (l * rl) * (k * rk);
     } else {
-      const float e = zl[i] - zk[i];
+      const float e = l - k;
       raw += e * e;
     }
+  };
+  if ((L & 3) == 0 && (ldz & 3) == 0) {  // 16-B loads: 4 elements per lane and step
+    for (int i = 4 * lane; i < L; i += 256) {
+      const float4 mu = *reinterpret_cast<const float4*>(msl + i);
+      const float4 s = *reinterpret_cast<const float4*>(msl + L + i);
+      const float4 l = *reinterpret_cast<const float4*>(zl + i);
+      const float4 r = *reinterpret_cast<const float4*>(zr + i);
+      const float4 k = *reinterpret_cast<const float4*>(zk + i);
+      term(mu.x, s.x, l.x, r.x, k.x, i);
+      term(mu.y, s.y, l.y, r.y, k.y, i + 1);
+      term(mu.z, s.z, l.z, r.z, k.z, i + 2);
+      term(mu.w, s.w, l.w, r.w, k.w, i + 3);
+    }
+  } else {
+    for (int i = lane; i < L; i += 64) term(msl[i], msl[L + i], zl[i], zr[i], zk[i], i);
   }
   for (int j = lane; j < nblk; j += 64) rp += rowpart[(size_t)b * nblk + j];
 #pragma unroll
@@ -503,6 +542,12 @@ hipError_t launch_normal(float* out, int slots, int B, int L, int Bg, int off, u
 
 hipError_t launch_latent_fwd(const float* ms, const float* eps, float* z, const Planes& zp, int B,
                              int L, int ldz, hipStream_t st) {
+  if (L % 4 == 0 && ldz % 4 == 0) {
+    const size_t n4 = (size_t)3 * B * (L / 4);
+    hipLaunchKernelGGL(latent_fwd4_kernel, dim3(nblocks(n4, 256)), dim3(256), 0, st, ms, eps, z, zp.p,
+                       zp.stride, zp.n, B, L, ldz);
+    return hipGetLastError();
+  }
   const size_t n = (size_t)3 * B * L;
   hipLaunchKernelGGL(latent_fwd_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, ms, eps, z, zp.p,
                      zp.stride, zp.n, B, L, ldz);
