@@ -9,8 +9,8 @@ reference is mounted; the GPU box only reads the committed files).
   overlap_micro.npz      the reference's ``overlap_micro.zip`` (100 lock/key pairs, 200x200
                          binary PNGs) as packed bits: data, not code.
   step_<flavour>.npz     oracle (float64) golden vectors for one training step of a tiny
-                         config per preset flavour: inputs, 5 losses, distance, g1, g2,
-                         post-Adam parameters.
+                         config per preset flavour (and the conv-encoder variant): inputs,
+                         5 losses, distance, g1, g2, post-Adam parameters.
 
 Usage: python tests/golden/make_golden.py [--reference /root/reference]
 """
@@ -36,6 +36,9 @@ FLAVOURS = {
     "9a_recip_cosine": dict(act="tanh", metric="cosine", reciprocal=True, deform_weight=10.0),
     "11a_recip_sqdiff_elu": dict(act="elu", metric="sqdiff", reciprocal=True, deform_weight=100.0),
     "sqdiff_tanh": dict(act="tanh", metric="sqdiff", reciprocal=False, deform_weight=10.0),
+    # conv-encoder variant (tower of 6b/net.py:50-60): image side a multiple of 4
+    "conv_recip_sqdiff": dict(act="tanh", metric="sqdiff", reciprocal=True, deform_weight=10.0,
+                              conv=True, image_size=12),
 }
 TINY = dict(image_size=10, enc=(24, 16), dec=(12, 14), latent=4, lr=(1e-3, 1e-4))
 TINY_B = 8
@@ -68,8 +71,12 @@ def pack_micro(path: str) -> dict:
             "shape": np.array(L.shape)}
 
 
+def golden_cfg(flav: dict) -> O.OracleConfig:
+    return O.OracleConfig(**dict(TINY, **flav))
+
+
 def step_golden(name: str, flav: dict) -> dict:
-    cfg = O.OracleConfig(**TINY, **flav)
+    cfg = golden_cfg(flav)
     P = O.init_params(cfg, seed=0, dtype=np.float64)
     rng = np.random.default_rng(7)
     for k in P:

@@ -15,8 +15,8 @@ STEPS = sorted(glob.glob(os.path.join(GOLD, "step_*.npz")))
 def load_step(path):
     z = np.load(path)
     name = os.path.basename(path)[5:-4]
-    from tests.golden.make_golden import FLAVOURS, TINY
-    cfg = O.OracleConfig(**TINY, **FLAVOURS[name])
+    from tests.golden.make_golden import FLAVOURS, golden_cfg
+    cfg = golden_cfg(FLAVOURS[name])
     get = lambda pre: {k[len(pre):]: z[k] for k in z.files if k.startswith(pre)}  # noqa: E731
     return cfg, z, get("P/"), get("g1/"), get("g2/"), get("Pn/")
 
@@ -51,4 +51,4 @@ def test_oracle_reproduces_golden_step(path):
         np.testing.assert_allclose(h2[k], g2[k], rtol=1e-10, atol=1e-14)
     for k in Pn:
         np.testing.assert_allclose(Pn2[k], Pn[k], rtol=1e-12)
-    assert len(STEPS) == 4
+    assert len(STEPS) == 5
