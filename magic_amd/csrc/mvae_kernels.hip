@@ -303,7 +303,7 @@ __global__ void metric_kernel(const float* __restrict__ z, int ldz, const float*
       raw += e * e;
     }
   };
-  if ((L & 3) == 0 && (ldz & 3) == 0) {  // 16-B loads: 4 elements per lane and step
+  if ((L & 3) == 0 && L >= 256 && (ldz & 3) == 0) {  // 16-B loads, 4 elements per lane (all lanes busy)
     for (int i = 4 * lane; i < L; i += 256) {
       const float4 mu = *reinterpret_cast<const float4*>(msl + i);
       const float4 s = *reinterpret_cast<const float4*>(msl + L + i);
