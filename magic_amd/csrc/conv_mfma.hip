@@ -34,7 +34,7 @@ constexpr int CH = 64, NT = 25;
 
 __device__ __forceinline__ int swz(int px) { return (px >> 1) & 7; }
 
-template <bool FWD, int NW, int TPB>
+template <bool FWD, int NW, int TPB, int FPW>
 __global__ __launch_bounds__(64 * NW) void conv2_mfma_kernel(const unsigned short* __restrict__ in,
                                                             const unsigned short* __restrict__ wimg,
                                                             const float* __restrict__ bias,
@@ -83,18 +83,19 @@ __global__ __launch_bounds__(64 * NW) void conv2_mfma_kernel(const unsigned shor
   put_w(wb);
   __syncthreads();
   const int nfr = (npx + 31) >> 5;
-  const bool has0 = wave < nfr, has1 = wave + NW < nfr;  // wave-uniform
-  int pb[2];
+  bool has[FPW];  // wave-uniform
+  int pb[FPW];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < FPW; ++i) {
+    has[i] = wave + NW * i < nfr;
     const int pl = (wave + NW * i) * 32 + (lane & 31);
     const int q = pl < npx ? pl : 0;
     pb[i] = (q / S1) * PW + q % S1;
   }
   const int h = lane >> 5;
-  f32x16 acc[2][2];
+  f32x16 acc[FPW][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FPW; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
@@ -110,9 +111,9 @@ __global__ __launch_bounds__(64 * NW) void conv2_mfma_kernel(const unsigned shor
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int c = 2 * ks + h;
-      bf16x8 fa[2], fb[2];
+      bf16x8 fa[FPW], fb[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < FPW; ++i) {
         const int px = pb[i] + toff;
         fa[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(patch + px * CH + 8 * (c ^ swz(px))));
       }
@@ -121,14 +122,12 @@ __global__ __launch_bounds__(64 * NW) void conv2_mfma_kernel(const unsigned shor
         const int n = nf * 32 + (lane & 31);
         fb[nf] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(wc + n * CH + 8 * (c ^ swz(n))));
       }
-      if (has0) {
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[0], acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[0], fb[1], acc[0][1], 0, 0, 0);
-      }
-      if (has1) {
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[0], acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[1], fb[1], acc[1][1], 0, 0, 0);
-      }
+#pragma unroll
+      for (int i = 0; i < FPW; ++i)
+        if (has[i]) {
+          acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[0], acc[i][0], 0, 0, 0);
+          acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[1], acc[i][1], 0, 0, 0);
+        }
     }
    }
     if (g + 1 < NG) put_w(wb + ((g + 1) & 1) * TPB * CH * CH);
@@ -137,8 +136,8 @@ __global__ __launch_bounds__(64 * NW) void conv2_mfma_kernel(const unsigned shor
   // C: row (pixel) (r&3) + 8(r>>2) + 4h of the fragment, column (channel) lane&31 + 32 nf
   const size_t obase = ibase + (size_t)y0 * S1 * CH;
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    if (!(i ? has1 : has0)) continue;
+  for (int i = 0; i < FPW; ++i) {
+    if (!has[i]) continue;
 #pragma unroll
     for (int nf = 0; nf < 2; ++nf) {
       const int n = nf * 32 + (lane & 31);
@@ -437,15 +436,15 @@ __global__ void conv2_wprep_kernel(const float* __restrict__ W, unsigned short* 
 }  // namespace
 
 // band rows of the forward / data-gradient kernel with nw waves (64 nw pixel slots)
-int conv2_mfma_band(int S1, int nw, int tpb) {
+int conv2_mfma_band(int S1, int nw, int tpb, int fpw) {
   const size_t wlds = (size_t)2 * tpb * CH * CH * 2;   // two slots of TPB taps
-  int br = std::max(1, std::min(S1, 64 * nw / S1));
+  int br = std::max(1, std::min(S1, 32 * nw * fpw / S1));
   while (br > 1 && (size_t)(br + 4) * (S1 + 4) * CH * 2 + wlds > 160 * 1024) --br;
   return br;
 }
 
-size_t conv2_mfma_lds(int S1, int nw, int tpb) {
-  const int br = conv2_mfma_band(S1, nw, tpb);
+size_t conv2_mfma_lds(int S1, int nw, int tpb, int fpw) {
+  const int br = conv2_mfma_band(S1, nw, tpb, fpw);
   return (size_t)(br + 4) * (S1 + 4) * CH * 2 + (size_t)2 * tpb * CH * CH * 2;
 }
 
@@ -467,22 +466,24 @@ hipError_t launch_conv2_mfma(const ConvTower& T, bool fwd, const unsigned short*
                              hipStream_t st) {
   const int nw = T.conv2_nw == 8 ? 8 : 4;
   const int tpb = nw == 8 && T.conv2_tpb == 2 ? 2 : 1;
-  const int br = conv2_mfma_band(T.S1, nw, tpb);
-  const size_t lds = conv2_mfma_lds(T.S1, nw, tpb);
+  const int fpw = nw == 4 && T.conv2_fpw == 4 ? 4 : 2;
+  const int br = conv2_mfma_band(T.S1, nw, tpb, fpw);
+  const size_t lds = conv2_mfma_lds(T.S1, nw, tpb, fpw);
   dim3 g((T.S1 + br - 1) / br, nimg);
   const float* bias = w2 + (size_t)NT * CH * CH;
-#define CONV2_LAUNCH(NW_, TPB_)                                                                     \
+#define CONV2_LAUNCH(NW_, TPB_, FPW_)                                                              \
   do {                                                                                             \
     if (fwd)                                                                                       \
-      hipLaunchKernelGGL((conv2_mfma_kernel<true, NW_, TPB_>), g, dim3(64 * NW_), lds, st, inb,    \
-                         wimg, bias, out, T.S1, br);                                               \
+      hipLaunchKernelGGL((conv2_mfma_kernel<true, NW_, TPB_, FPW_>), g, dim3(64 * NW_), lds, st,   \
+                         inb, wimg, bias, out, T.S1, br);                                          \
     else                                                                                           \
-      hipLaunchKernelGGL((conv2_mfma_kernel<false, NW_, TPB_>), g, dim3(64 * NW_), lds, st, inb,   \
-                         wimg, bias, out, T.S1, br);                                               \
+      hipLaunchKernelGGL((conv2_mfma_kernel<false, NW_, TPB_, FPW_>), g, dim3(64 * NW_), lds, st,  \
+                         inb, wimg, bias, out, T.S1, br);                                          \
   } while (0)
-  if (nw == 8 && tpb == 2) CONV2_LAUNCH(8, 2);
-  else if (nw == 8) CONV2_LAUNCH(8, 1);
-  else CONV2_LAUNCH(4, 1);
+  if (nw == 8 && tpb == 2) CONV2_LAUNCH(8, 2, 2);
+  else if (nw == 8) CONV2_LAUNCH(8, 1, 2);
+  else if (fpw == 4) CONV2_LAUNCH(4, 1, 4);
+  else CONV2_LAUNCH(4, 1, 2);
 #undef CONV2_LAUNCH
   return hipGetLastError();
 }

@@ -477,6 +477,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     // kernel-shape A/B switches (diagnostics): MVAE_CONV2_NW=4, MVAE_CONV2_TPB=2, MVAE_CONV2_WG=4
     if (const char* nw = std::getenv("MVAE_CONV2_NW"); nw && *nw == '4') T.conv2_nw = 4;
     if (const char* tp = std::getenv("MVAE_CONV2_TPB"); tp && *tp == '2') T.conv2_tpb = 2;
+    if (const char* fp = std::getenv("MVAE_CONV2_FPW"); fp && *fp == '4') T.conv2_fpw = 4;
     if (const char* wg = std::getenv("MVAE_CONV2_WG"); wg && *wg == '4') T.conv2_wg8 = false;
     ALLOC(c->xf, 3 * B * c->ldf);
     ALLOC(c->dxf, 4 * B * c->ldf);
@@ -1410,6 +1411,7 @@ extern "C" int mvae_debug_conv2(int S1, int B, int mode, int mfma, const float* 
   T.mfma = mfma != 0;
   if (const char* nw = std::getenv("MVAE_CONV2_NW"); nw && *nw == '4') T.conv2_nw = 4;
   if (const char* tp = std::getenv("MVAE_CONV2_TPB"); tp && *tp == '2') T.conv2_tpb = 2;
+  if (const char* fp = std::getenv("MVAE_CONV2_FPW"); fp && *fp == '4') T.conv2_fpw = 4;
   if (const char* wg = std::getenv("MVAE_CONV2_WG"); wg && *wg == '4') T.conv2_wg8 = false;
   const size_t img = (size_t)S1 * S1 * 64;
   const int B2 = 2 * B;

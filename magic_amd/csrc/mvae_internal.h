@@ -150,6 +150,7 @@ struct ConvTower {
   bool mfma = false;               // conv2 on bf16 MFMA (bf16 mode)
   int conv2_nw = 8;                // waves per workgroup of the conv2 forward / data-gradient kernel
   int conv2_tpb = 1;               // ... and taps per weight slot (one barrier per slot)
+  int conv2_fpw = 2;               // ... and 32-pixel M-fragments per wave
   bool conv2_wg8 = true;           // weight gradient: 8-wave all-n workgroups (else 4-wave quarters)
 };
 hipError_t launch_conv1_fwd(const ConvTower& T, const float* xs, int ldx, const float* w1, int nimg,
@@ -168,8 +169,8 @@ hipError_t launch_conv2_mfma(const ConvTower& T, bool fwd, const unsigned short*
                              const unsigned short* wimg, const float* w2, float* out, int nimg,
                              hipStream_t st);
 hipError_t launch_conv2_wgrad_mfma(const ConvTower& T, int B, hipStream_t st);
-int conv2_mfma_band(int S1, int nw, int tpb);
-size_t conv2_mfma_lds(int S1, int nw, int tpb);
+int conv2_mfma_band(int S1, int nw, int tpb, int fpw);
+size_t conv2_mfma_lds(int S1, int nw, int tpb, int fpw);
 int conv2_wgrad_rows(int S1);
 size_t conv2_wgrad_lds(int S1);
 
