@@ -353,8 +353,9 @@ def cpu_baseline(cfg, dev, seconds: float):
     v_c1, n_c1, t_c1 = timed(X1, A1, E1, seconds)
     with threadpool_limits(1):
         v_c1_1, n_c1_1, t_c1_1 = timed(X1, A1, E1, seconds)
-    # the GPU-batch workload (the bench's own step shape), all threads, >= 2 steps
-    Bg = cfg.batch
+    # the GPU-batch workload (the bench's own step shape), all threads, >= 2 steps; the conv
+    # oracle's im2col would hold 3*B*2500 x 1600 values: its sample is 64 pairs of that shape
+    Bg = min(cfg.batch, 64) if cfg.conv else cfg.batch
     xg, ag = synthetic_batch(Bg, cfg.image_size, seed=4243, device=dev)
     Eg = np.random.default_rng(3).standard_normal((3, Bg, cfg.latent)).astype(np.float32)
     v_g, n_g, t_g = timed(xg.cpu().numpy(), ag.cpu().numpy(), Eg, seconds)
