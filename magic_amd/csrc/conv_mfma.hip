@@ -51,7 +51,7 @@ __global__ __launch_bounds__(64 * NW) void conv2_mfma_kernel(const unsigned shor
   const size_t ibase = (size_t)img * S1 * S1 * CH;
   // a tap's 64x64 slice = 512 16-B chunks, 512 / (64 NW) per thread: chunk q -> n = q/8, k chunk q%8.
   // TPB taps per LDS slot (one barrier per slot); two slots
-  constexpr int NT_ = 64 * NW, WCH = 512 / NT_, NG = (NT + TPB - 1) / TPB;
+  constexpr int NT_ = 64 * NW, WCH = NT_ >= 512 ? 1 : 512 / NT_, NG = (NT + TPB - 1) / TPB;
   int4 wr[TPB][WCH];
   auto get_w = [&](int g) {
 #pragma unroll
@@ -59,7 +59,8 @@ __global__ __launch_bounds__(64 * NW) void conv2_mfma_kernel(const unsigned shor
 #pragma unroll
       for (int u = 0; u < WCH; ++u) {
         const int t = g * TPB + j;
-        if (t < NT) wr[j][u] = *reinterpret_cast<const int4*>(wimg + (size_t)t * CH * CH + 8 * (tid + NT_ * u));
+        if (t < NT && tid + NT_ * u < 512)
+          wr[j][u] = *reinterpret_cast<const int4*>(wimg + (size_t)t * CH * CH + 8 * (tid + NT_ * u));
       }
   };
   get_w(0);
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(64 * NW) void conv2_mfma_kernel(const unsigned shor
 #pragma unroll
       for (int u = 0; u < WCH; ++u) {
         const int q = tid + NT_ * u, n = q >> 3, c = q & 7;
-        *reinterpret_cast<int4*>(dst + j * CH * CH + n * CH + 8 * (c ^ swz(n))) = wr[j][u];
+        if (q < 512) *reinterpret_cast<int4*>(dst + j * CH * CH + n * CH + 8 * (c ^ swz(n))) = wr[j][u];
       }
   };
   put_w(wb);
@@ -464,9 +465,9 @@ hipError_t launch_conv2_wprep(const ConvTower& T, const float* w2, hipStream_t s
 hipError_t launch_conv2_mfma(const ConvTower& T, bool fwd, const unsigned short* inb,
                              const unsigned short* wimg, const float* w2, float* out, int nimg,
                              hipStream_t st) {
-  const int nw = T.conv2_nw == 8 ? 8 : 4;
+  const int nw = T.conv2_nw == 16 ? 16 : (T.conv2_nw == 8 ? 8 : 4);
   const int tpb = nw == 8 && T.conv2_tpb == 2 ? 2 : 1;
-  const int fpw = nw == 4 && T.conv2_fpw == 4 ? 4 : 2;
+  const int fpw = nw == 16 ? 1 : (nw == 4 && T.conv2_fpw == 4 ? 4 : 2);
   const int br = conv2_mfma_band(T.S1, nw, tpb, fpw);
   const size_t lds = conv2_mfma_lds(T.S1, nw, tpb, fpw);
   dim3 g((T.S1 + br - 1) / br, nimg);
@@ -480,7 +481,8 @@ hipError_t launch_conv2_mfma(const ConvTower& T, bool fwd, const unsigned short*
       hipLaunchKernelGGL((conv2_mfma_kernel<false, NW_, TPB_, FPW_>), g, dim3(64 * NW_), lds, st,  \
                          inb, wimg, bias, out, T.S1, br);                                          \
   } while (0)
-  if (nw == 8 && tpb == 2) CONV2_LAUNCH(8, 2, 2);
+  if (nw == 16) CONV2_LAUNCH(16, 1, 1);
+  else if (nw == 8 && tpb == 2) CONV2_LAUNCH(8, 2, 2);
   else if (nw == 8) CONV2_LAUNCH(8, 1, 2);
   else if (fpw == 4) CONV2_LAUNCH(4, 1, 4);
   else CONV2_LAUNCH(4, 1, 2);
