@@ -297,6 +297,8 @@ __global__ __launch_bounds__(512) void conv2_wgrad_mfma8_kernel(const unsigned s
   const int nslot = ((R * S1 + 15) / 16) * 16;
   unsigned short* ap = lds;                      // [(R+4)*PW][32]
   unsigned short* dp = lds + (R + 4) * PW * 32;  // [nslot][64], 64-B halves swapped by (p>>1)&1
+  // patch row of each pixel slot of a row block: ptab[p] = (p / S1) * PW + p % S1
+  int* ptab = reinterpret_cast<int*>(dp + ((R * S1 + 15) / 16 * 16) * 64);
   const int id = blockIdx.x;
   const int xcd = id & 7, kh = (id >> 3) & 1, cgi = (id >> 4) * 8 + xcd;
   if (cgi >= 2 * nchunk) return;                 // workgroup-uniform
@@ -321,6 +323,7 @@ __global__ __launch_bounds__(512) void conv2_wgrad_mfma8_kernel(const unsigned s
 #pragma unroll
     for (int r = 0; r < 16; ++r) accb[n2][r] = 0.f;
   const bool dobias = kh == 0 && wave == 7;      // wave 7 holds 3 taps: room for the bias rows
+  for (int p = tid; p < nslot; p += 512) ptab[p] = (p / S1) * PW + p % S1;   // read after 1st barrier
   const int i16 = lane & 15, q = i16 >> 2, pq = i16 & 3, h = lane >> 5, g1 = (lane >> 4) & 1;
   const int col = 16 * g1 + 4 * pq;
   bf16x8 ones;
@@ -375,7 +378,7 @@ __global__ __launch_bounds__(512) void conv2_wgrad_mfma8_kernel(const unsigned s
     for (int s = 0; s < nslot / 16; ++s) {
       const int klo = 16 * s + 8 * h + q, khi = klo + 4;
       const int plo = klo < npx ? klo : 0, phi = khi < npx ? khi : 0;
-      const int alo = (plo / S1) * PW + plo % S1, ahi = (phi / S1) * PW + phi % S1;
+      const int alo = ptab[plo], ahi = ptab[phi];
       bf16x8 fb[2];
 #pragma unroll
       for (int n2 = 0; n2 < 2; ++n2) {
@@ -498,7 +501,8 @@ hipError_t launch_conv2_wgrad_mfma(const ConvTower& T, int B, hipStream_t st) {
   const int chunks = (R + 4) * (T.S1 + 4) * 4;   // 16-B chunks of the A image per thread block
   if (T.conv2_wg8 && (size_t)((R * T.S1 + 15) / 16 * 16) * 8 <= 4 * 512) {
     const int g16 = (2 * nchunk + 7) / 8;
-    const size_t lds = ((size_t)(R + 4) * (T.S1 + 4) * 32 + (size_t)(R * T.S1 + 15) / 16 * 16 * 64) * 2;
+    const size_t nsl = (size_t)(R * T.S1 + 15) / 16 * 16;
+    const size_t lds = ((size_t)(R + 4) * (T.S1 + 4) * 32 + nsl * 64) * 2 + nsl * 4;
     if (chunks <= 4 * 512)
       hipLaunchKernelGGL(conv2_wgrad_mfma8_kernel<4>, dim3(g16 * 16), dim3(512), lds, st, T.n1b, T.da2b, T.S1,
                          R, B2, nchunk, ipc, T.slab);
