@@ -330,6 +330,14 @@ __global__ __launch_bounds__(512) void conv2_wgrad_mfma8_kernel(const unsigned s
 #pragma unroll
   for (int e = 0; e < 8; ++e) ones[e] = (__bf16)1.0f;
   int4 ra[NA], rd[4];
+  // this thread's A-image chunks sit at the same (patch row, column) in every row block
+  int arow[NA], acol[NA];
+#pragma unroll
+  for (int u = 0; u < NA; ++u) {
+    const int px = (tid + 512 * u) >> 2;
+    arow[u] = px / PW;
+    acol[u] = px - arow[u] * PW - 2;
+  }
   auto fetch = [&](int b) {
     const int j = j0 + b / nrb, r0 = (b % nrb) * R;
     const int f = j < B2 ? j : j - B2 / 2;
@@ -339,8 +347,8 @@ __global__ __launch_bounds__(512) void conv2_wgrad_mfma8_kernel(const unsigned s
       const int i = tid + 512 * u;
       ra[u] = make_int4(0, 0, 0, 0);
       if (i < nA) {
-        const int px = i >> 2, c = i & 3;
-        const int y = r0 - 2 + px / PW, x = px % PW - 2;
+        const int c = i & 3;
+        const int y = r0 - 2 + arow[u], x = acol[u];
         if (y >= 0 && y < S1 && x >= 0 && x < S1)
           ra[u] = *reinterpret_cast<const int4*>(inb + ((size_t)f * np1 + y * S1 + x) * CH + 32 * kh + 8 * c);
       }
