@@ -72,7 +72,10 @@ def parse_args(argv=None):
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launcher / data-parallel / timing / JSON path "
                          "(gloo, a stand-in engine; no GPU, no kernels, not a measurement)")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.region_steps < 1:
+        ap.error("--region-steps must be >= 1 (the roofline's dominant kernel comes from the region pass)")
+    return args
 
 
 # ------------------------------------------------------------------------ launcher
