@@ -11,6 +11,9 @@
 // 16 distinct bank slots. 4 waves x (2 M-fragments of 32 pixels) x (2 N-fragments): 256 pixel
 // slots; for S1 = 50 a band is 5 rows = 250 pixels. LDS 78.6 KB: two workgroups per CU, so one
 // stages its patch while the other computes.
+// conv2_mfma_half_kernel (the default) walks the input channels in two halves of 32 with
+// 8 waves and 10-row bands at S1 = 50: 56 KB of LDS, two workgroups per CU (the full-channel
+// 8-wave form needs 113 KB and runs alone on its CU, every per-tap barrier exposed).
 //
 // conv2_wgrad_mfma_kernel — dW[t][k][n] = sum_p in[p + t][k] d[p][n]: K = pixels, so both
 // operands are pixel-major ([pixel][channel] rows) and are read with ds_read_b64_tr_b16 (each
@@ -135,6 +138,119 @@ __global__ __launch_bounds__(64 * NW) void conv2_mfma_kernel(const unsigned shor
     __syncthreads();
   }
   // C: row (pixel) (r&3) + 8(r>>2) + 4h of the fragment, column (channel) lane&31 + 32 nf
+  const size_t obase = ibase + (size_t)y0 * S1 * CH;
+#pragma unroll
+  for (int i = 0; i < FPW; ++i) {
+    if (!has[i]) continue;
+#pragma unroll
+    for (int nf = 0; nf < 2; ++nf) {
+      const int n = nf * 32 + (lane & 31);
+      const float b = FWD ? bias[n] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int pl = (wave + NW * i) * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (pl >= npx) continue;
+        float v = acc[i][nf][r];
+        if (FWD) v = fmaxf(v + b, 0.f);
+        out[obase + (size_t)pl * CH + n] = v;
+      }
+    }
+  }
+}
+
+// Channel-half form of conv2_mfma_kernel (8 waves, 2 M-fragments each): the 64 input channels
+// are walked in two halves of 32, each a full pass over the 25 taps with the band patch and the
+// kernel slices of that half only (64-B pixel / kernel rows, 16-B chunks swizzled by (row>>2)&3:
+// 16 consecutive rows of one chunk column hit 16 distinct slots of a 256-B bank row). LDS is
+// half of the full-channel form's (56 KB at S1 = 50), so two workgroups share a CU and one's
+// per-tap barrier and LDS latency overlap the other's MFMAs; the accumulators carry over.
+__device__ __forceinline__ int swz4(int r) { return (r >> 2) & 3; }
+
+template <bool FWD>
+__global__ __launch_bounds__(512, 2) void conv2_mfma_half_kernel(const unsigned short* __restrict__ in,
+                                                                 const unsigned short* __restrict__ wimg,
+                                                                 const float* __restrict__ bias,
+                                                                 float* __restrict__ out, int S1, int BR) {
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
+  constexpr int NW = 8, FPW = 2, HC = 32;
+  const int PW = S1 + 4, PR = BR + 4;
+  unsigned short* patch = lds;                 // [PR*PW][32]
+  unsigned short* wb = lds + PR * PW * HC;     // 2 slots x [64 n][32 k]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int img = blockIdx.y;
+  const int y0 = blockIdx.x * BR;
+  const int rows = min(BR, S1 - y0);
+  const int npx = rows * S1;
+  const size_t ibase = (size_t)img * S1 * S1 * CH;
+  // a tap's half slice = 256 16-B chunks: thread q < 256 -> n = q / 4, chunk q % 4
+  int4 wr = make_int4(0, 0, 0, 0);
+  auto get_w = [&](int hh, int t) {
+    if (tid < 256) wr = *reinterpret_cast<const int4*>(wimg + (size_t)t * CH * CH + (tid >> 2) * CH + HC * hh + 8 * (tid & 3));
+  };
+  auto put_w = [&](unsigned short* dst) {
+    const int n = tid >> 2, c = tid & 3;
+    if (tid < 256) *reinterpret_cast<int4*>(dst + n * HC + 8 * (c ^ swz4(n))) = wr;
+  };
+  const int nfr = (npx + 31) >> 5;
+  bool has[FPW];  // wave-uniform
+  int pb[FPW];
+#pragma unroll
+  for (int i = 0; i < FPW; ++i) {
+    has[i] = wave + NW * i < nfr;
+    const int pl = (wave + NW * i) * 32 + (lane & 31);
+    const int q = pl < npx ? pl : 0;
+    pb[i] = (q / S1) * PW + q % S1;
+  }
+  const int h = lane >> 5;
+  f32x16 acc[FPW][2];
+#pragma unroll
+  for (int i = 0; i < FPW; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  for (int hh = 0; hh < 2; ++hh) {
+    // every read of the previous half ended before the tap loop's last barrier
+    get_w(hh, 0);
+    for (int i = tid; i < PR * PW * 4; i += 64 * NW) {
+      const int px = i >> 2, c = i & 3;
+      const int y = y0 - 2 + px / PW, x = px % PW - 2;
+      int4 v = make_int4(0, 0, 0, 0);
+      if (y >= 0 && y < S1 && x >= 0 && x < S1)
+        v = *reinterpret_cast<const int4*>(in + ibase + ((size_t)y * S1 + x) * CH + HC * hh + 8 * c);
+      *reinterpret_cast<int4*>(patch + px * HC + 8 * (c ^ swz4(px))) = v;
+    }
+    put_w(wb);
+    __syncthreads();
+    for (int t = 0; t < NT; ++t) {
+      if (t + 1 < NT) get_w(hh, t + 1);
+      const unsigned short* wc = wb + (t & 1) * CH * HC;
+      const int toff = (t / 5) * PW + t % 5;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = 2 * ks + h;
+        bf16x8 fa[FPW], fb[2];
+#pragma unroll
+        for (int i = 0; i < FPW; ++i) {
+          const int px = pb[i] + toff;
+          fa[i] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(patch + px * HC + 8 * (c ^ swz4(px))));
+        }
+#pragma unroll
+        for (int nf = 0; nf < 2; ++nf) {
+          const int n = nf * 32 + (lane & 31);
+          fb[nf] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const s16x8*>(wc + n * HC + 8 * (c ^ swz4(n))));
+        }
+#pragma unroll
+        for (int i = 0; i < FPW; ++i)
+          if (has[i]) {
+            acc[i][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[0], acc[i][0], 0, 0, 0);
+            acc[i][1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[1], acc[i][1], 0, 0, 0);
+          }
+      }
+      if (t + 1 < NT) put_w(wb + ((t + 1) & 1) * CH * HC);
+      __syncthreads();
+    }
+  }
   const size_t obase = ibase + (size_t)y0 * S1 * CH;
 #pragma unroll
   for (int i = 0; i < FPW; ++i) {
@@ -492,6 +608,17 @@ hipError_t launch_conv2_mfma(const ConvTower& T, bool fwd, const unsigned short*
       hipLaunchKernelGGL((conv2_mfma_kernel<false, NW_, TPB_, FPW_>), g, dim3(64 * NW_), lds, st,  \
                          inb, wimg, bias, out, T.S1, br);                                          \
   } while (0)
+  if (T.conv2_half) {
+    // channel-half form: band of 512 pixel slots, 2 workgroups per CU
+    const int hbr = std::max(1, std::min(T.S1, 512 / T.S1));
+    const size_t hlds = ((size_t)(hbr + 4) * (T.S1 + 4) * 32 + (size_t)2 * CH * 32) * 2;
+    dim3 hg((T.S1 + hbr - 1) / hbr, nimg);
+    if (fwd)
+      hipLaunchKernelGGL((conv2_mfma_half_kernel<true>), hg, dim3(512), hlds, st, inb, wimg, bias, out, T.S1, hbr);
+    else
+      hipLaunchKernelGGL((conv2_mfma_half_kernel<false>), hg, dim3(512), hlds, st, inb, wimg, bias, out, T.S1, hbr);
+    return hipGetLastError();
+  }
   if (nw == 16) CONV2_LAUNCH(16, 1, 1);
   else if (nw == 8 && tpb == 2) CONV2_LAUNCH(8, 2, 2);
   else if (nw == 8) CONV2_LAUNCH(8, 1, 2);

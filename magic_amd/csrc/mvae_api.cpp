@@ -474,11 +474,13 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     ConvTower& T = c->tower;
     const size_t a1 = (size_t)T.S1 * T.S1 * 64, a2n = (size_t)T.S2 * T.S2 * 64;
     T.mfma = cfg->precision == MVAE_PREC_BF16;
-    // kernel-shape A/B switches (diagnostics): MVAE_CONV2_NW=4, MVAE_CONV2_TPB=2, MVAE_CONV2_WG=4
+    // kernel-shape A/B switches (diagnostics): MVAE_CONV2_HALF=0 (full-channel forward / data
+    // gradient kernel, shaped by MVAE_CONV2_NW=4|16, MVAE_CONV2_TPB=2, MVAE_CONV2_FPW=4), MVAE_CONV2_WG=4
     if (const char* nw = std::getenv("MVAE_CONV2_NW"); nw && (*nw == '4' || nw[0] == '1')) T.conv2_nw = *nw == '4' ? 4 : 16;
     if (const char* tp = std::getenv("MVAE_CONV2_TPB"); tp && *tp == '2') T.conv2_tpb = 2;
     if (const char* fp = std::getenv("MVAE_CONV2_FPW"); fp && *fp == '4') T.conv2_fpw = 4;
     if (const char* wg = std::getenv("MVAE_CONV2_WG"); wg && *wg == '4') T.conv2_wg8 = false;
+    if (const char* hf = std::getenv("MVAE_CONV2_HALF"); hf && *hf == '0') T.conv2_half = false;
     ALLOC(c->xf, 3 * B * c->ldf);
     ALLOC(c->dxf, 4 * B * c->ldf);
     ALLOC(T.p1, 3 * B * a1);
@@ -1413,6 +1415,7 @@ extern "C" int mvae_debug_conv2(int S1, int B, int mode, int mfma, const float* 
   if (const char* tp = std::getenv("MVAE_CONV2_TPB"); tp && *tp == '2') T.conv2_tpb = 2;
   if (const char* fp = std::getenv("MVAE_CONV2_FPW"); fp && *fp == '4') T.conv2_fpw = 4;
   if (const char* wg = std::getenv("MVAE_CONV2_WG"); wg && *wg == '4') T.conv2_wg8 = false;
+  if (const char* hf = std::getenv("MVAE_CONV2_HALF"); hf && *hf == '0') T.conv2_half = false;
   const size_t img = (size_t)S1 * S1 * 64;
   const int B2 = 2 * B;
   T.nchunk2 = std::min(B2, 32);

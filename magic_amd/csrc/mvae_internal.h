@@ -151,6 +151,7 @@ struct ConvTower {
   int conv2_nw = 8;                // waves per workgroup of the conv2 forward / data-gradient kernel
   int conv2_tpb = 1;               // ... and taps per weight slot (one barrier per slot)
   int conv2_fpw = 2;               // ... and 32-pixel M-fragments per wave
+  bool conv2_half = true;          // forward / data gradient: channel-half kernel (2 WGs per CU)
   bool conv2_wg8 = true;           // weight gradient: 8-wave all-n workgroups (else 4-wave quarters)
 };
 hipError_t launch_conv1_fwd(const ConvTower& T, const float* xs, int ldx, const float* w1, int nimg,

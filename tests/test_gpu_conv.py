@@ -168,3 +168,12 @@ def test_conv2_kernel(mode, mfma, S1, B):
     got = out.cpu().numpy().astype(np.float64).reshape(ref.shape)
     err = np.abs(got - ref).max() / max(np.abs(mag).max(), 1e-30)
     assert err <= 2e-6, err
+
+
+@pytest.mark.parametrize("mode", [0, 1], ids=["fwd", "dgrad"])
+def test_conv2_kernel_full_channel_form(mode, monkeypatch):
+    """The full-channel forward / data-gradient kernel (MVAE_CONV2_HALF=0; the default is the
+    channel-half form) to the same bound."""
+    monkeypatch.setenv("MVAE_CONV2_HALF", "0")
+    test_conv2_kernel(mode, 1, 50, 1)
+
