@@ -239,8 +239,11 @@ __global__ __launch_bounds__(256) void lrn2_pool2_fwd_kernel(const float* __rest
 }
 
 // ---------------------------------------------------------------- pool2 + LRN2 + ReLU (backward)
-// One wave per (backward image, pooled pixel): dxf -> the window's argmax pixel -> LRNGrad
-// -> ReLU mask; every pixel of the window is written (zeros off the argmax).
+// One wave per PPW (backward image, pooled pixel) pairs: dxf -> the window's argmax pixel ->
+// LRNGrad -> ReLU mask; every pixel of the window is written (zeros off the argmax). The loads
+// of all PPW pooled pixels are issued before any of them is used (the kernel is bound by load
+// latency: one pooled pixel per wave left its waves waiting 77 % of their cycles).
+constexpr int PPW = 2;
 __global__ __launch_bounds__(256) void pool2_bwd_kernel(const float* __restrict__ dxf, int ldf,
                                                         const float* __restrict__ a2,
                                                         const unsigned char* __restrict__ arg2, int S1,
@@ -248,27 +251,40 @@ __global__ __launch_bounds__(256) void pool2_bwd_kernel(const float* __restrict_
                                                         unsigned short* __restrict__ da2b) {
   const int lane = threadIdx.x & 63;
   const int S2 = S1 / 2;
-  const long long P = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (P >= (long long)nimg * S2 * S2) return;
-  const int j = (int)(P / (S2 * S2));
-  const int qq = (int)(P - (long long)j * S2 * S2);
-  const int qy = qq / S2, qx = qq - qy * S2;
-  const int f = remap(j, B2);
-  const float g = dxf[(size_t)j * ldf + (size_t)qq * CH + lane];
-  const int ar = arg2[((size_t)f * S2 * S2 + qq) * CH + lane];
-  const float* src = a2 + (size_t)f * S1 * S1 * CH;
+  const long long NP = (long long)nimg * S2 * S2;
+  const long long P0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * PPW;
+  if (P0 >= NP) return;
+  float g[PPW], a[PPW][4];
+  int ar[PPW];
+  size_t obase[PPW];
+  int pw[PPW];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const size_t pix = (size_t)(2 * qy + (q >> 1)) * S1 + 2 * qx + (q & 1);
-    const float a = src[pix * CH + lane];
-    const float dn = ar == q ? g : 0.f;
-    float d = 0.f;
-    if (__ballot(dn != 0.f)) d = lrn_bwd(a, dn, lane);
-    d = a > 0.f ? d : 0.f;
-    const size_t o = ((size_t)j * S1 * S1 + pix) * CH + lane;
-    if (da2) da2[o] = d;
-    if (da2b) da2b[o] = bf16_bits(d);
+  for (int u = 0; u < PPW; ++u) {
+    const long long P = P0 + u < NP ? P0 + u : NP - 1;   // a tail duplicate writes the same values
+    const int j = (int)(P / (S2 * S2));
+    const int qq = (int)(P - (long long)j * S2 * S2);
+    const int qy = qq / S2, qx = qq - qy * S2;
+    const int f = remap(j, B2);
+    g[u] = dxf[(size_t)j * ldf + (size_t)qq * CH + lane];
+    ar[u] = arg2[((size_t)f * S2 * S2 + qq) * CH + lane];
+    const float* src = a2 + (size_t)f * S1 * S1 * CH;
+    pw[u] = (2 * qy) * S1 + 2 * qx;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) a[u][q] = src[(size_t)(pw[u] + (q >> 1) * S1 + (q & 1)) * CH + lane];
+    obase[u] = (size_t)j * S1 * S1;
   }
+#pragma unroll
+  for (int u = 0; u < PPW; ++u)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float dn = ar[u] == q ? g[u] : 0.f;
+      float d = 0.f;
+      if (__ballot(dn != 0.f)) d = lrn_bwd(a[u][q], dn, lane);
+      d = a[u][q] > 0.f ? d : 0.f;
+      const size_t o = (obase[u] + pw[u] + (q >> 1) * S1 + (q & 1)) * CH + lane;
+      if (da2) da2[o] = d;
+      if (da2b) da2b[o] = bf16_bits(d);
+    }
 }
 
 // ---------------------------------------------------------------- conv1 weight gradient
@@ -508,7 +524,7 @@ hipError_t launch_lrn2_pool2_fwd(const ConvTower& T, int nimg, float* xf, int ld
 }
 
 hipError_t launch_pool2_bwd(const ConvTower& T, const float* dxf, int ldf, int B, hipStream_t st) {
-  const size_t waves = (size_t)4 * B * T.S2 * T.S2;
+  const size_t waves = ((size_t)4 * B * T.S2 * T.S2 + PPW - 1) / PPW;
   hipLaunchKernelGGL(pool2_bwd_kernel, dim3(nblk(waves, 4)), dim3(256), 0, st, dxf, ldf, T.a2, T.arg2,
                      T.S1, 4 * B, 2 * B, T.da2, T.da2b);
   return hipGetLastError();
