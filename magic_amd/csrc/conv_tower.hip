@@ -210,32 +210,50 @@ __global__ __launch_bounds__(256) void conv2_valu_kernel(const float* __restrict
 }
 
 // ---------------------------------------------------------------- LRN2 + pool2 (forward)
-// One wave per pooled pixel: LRN of the four window pixels, first max -> the layer-0 operand
-// row (feature (qy*S2 + qx)*64 + c; fp32 and/or bf16 planes) and the window position.
+// One wave per FPP pooled pixels (loads of all of them issued first): LRN of the four window
+// pixels, first max -> the layer-0 operand row (feature (qy*S2 + qx)*64 + c; fp32 and/or bf16
+// planes) and the window position.
+constexpr int FPP = 2;
 __global__ __launch_bounds__(256) void lrn2_pool2_fwd_kernel(const float* __restrict__ a2, int S1, int nimg,
                                                              float* __restrict__ xf, int ldf, int f32,
                                                              unsigned short* __restrict__ xfp, long long pstride,
                                                              int np, unsigned char* __restrict__ arg2) {
   const int lane = threadIdx.x & 63;
   const int S2 = S1 / 2;
-  const long long P = (long long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (P >= (long long)nimg * S2 * S2) return;
-  const int img = (int)(P / (S2 * S2));
-  const int qq = (int)(P - (long long)img * S2 * S2);
-  const int qy = qq / S2, qx = qq - qy * S2;
-  const float* src = a2 + (size_t)img * S1 * S1 * CH;
-  float best = -INFINITY;
-  int arg = 0;
+  const long long NP = (long long)nimg * S2 * S2;
+  const long long P0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * FPP;
+  if (P0 >= NP) return;
+  float a[FPP][4];
+  long long Pu[FPP];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int y = 2 * qy + (q >> 1), x = 2 * qx + (q & 1);
-    const float v = lrn_fwd(src[((size_t)y * S1 + x) * CH + lane], lane);
-    if (v > best) { best = v; arg = q; }
+  for (int u = 0; u < FPP; ++u) {
+    const long long P = P0 + u < NP ? P0 + u : NP - 1;   // a tail duplicate writes the same values
+    Pu[u] = P;
+    const int img = (int)(P / (S2 * S2));
+    const int qq = (int)(P - (long long)img * S2 * S2);
+    const int qy = qq / S2, qx = qq - qy * S2;
+    const float* src = a2 + (size_t)img * S1 * S1 * CH;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      a[u][q] = src[((size_t)(2 * qy + (q >> 1)) * S1 + 2 * qx + (q & 1)) * CH + lane];
   }
-  const size_t o = (size_t)img * ldf + (size_t)qq * CH + lane;
-  if (f32) xf[o] = best;
-  if (xfp) put_planes(xfp, pstride, np, o, best);
-  arg2[(size_t)P * CH + lane] = (unsigned char)arg;
+#pragma unroll
+  for (int u = 0; u < FPP; ++u) {
+    float best = -INFINITY;
+    int arg = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float v = lrn_fwd(a[u][q], lane);
+      if (v > best) { best = v; arg = q; }
+    }
+    const long long P = Pu[u];
+    const int img = (int)(P / (S2 * S2));
+    const int qq = (int)(P - (long long)img * S2 * S2);
+    const size_t o = (size_t)img * ldf + (size_t)qq * CH + lane;
+    if (f32) xf[o] = best;
+    if (xfp) put_planes(xfp, pstride, np, o, best);
+    arg2[(size_t)P * CH + lane] = (unsigned char)arg;
+  }
 }
 
 // ---------------------------------------------------------------- pool2 + LRN2 + ReLU (backward)
@@ -243,7 +261,7 @@ __global__ __launch_bounds__(256) void lrn2_pool2_fwd_kernel(const float* __rest
 // LRNGrad -> ReLU mask; every pixel of the window is written (zeros off the argmax). The loads
 // of all PPW pooled pixels are issued before any of them is used (the kernel is bound by load
 // latency: one pooled pixel per wave left its waves waiting 77 % of their cycles).
-constexpr int PPW = 2;
+constexpr int PPW = 4;
 __global__ __launch_bounds__(256) void pool2_bwd_kernel(const float* __restrict__ dxf, int ldf,
                                                         const float* __restrict__ a2,
                                                         const unsigned char* __restrict__ arg2, int S1,
@@ -517,7 +535,7 @@ hipError_t launch_conv2(const ConvTower& T, bool fwd, const float* in, const uns
 
 hipError_t launch_lrn2_pool2_fwd(const ConvTower& T, int nimg, float* xf, int ldf, int f32,
                                  const Planes& xfp, hipStream_t st) {
-  const size_t waves = (size_t)nimg * T.S2 * T.S2;
+  const size_t waves = ((size_t)nimg * T.S2 * T.S2 + FPP - 1) / FPP;
   hipLaunchKernelGGL(lrn2_pool2_fwd_kernel, dim3(nblk(waves, 4)), dim3(256), 0, st, T.a2, T.S1, nimg, xf,
                      ldf, f32, xfp.p, xfp.stride, xfp.n, T.arg2);
   return hipGetLastError();
