@@ -93,7 +93,7 @@ __device__ __forceinline__ void put_planes(unsigned short* p, long long ps, int 
 // first-max pooling, then LRN across the lanes. w: conv1 block [26][64] (25 taps, bias row).
 // Writes p1 (pooled, for LRN1's backward), arg1 (window position of the max), n1 (conv2's
 // input) and, when n1b, its bf16 image.
-constexpr int SEG_MAX = 32;
+constexpr int SEG_MAX = 64;
 __global__ __launch_bounds__(256) void conv1_fwd_kernel(const float* __restrict__ xs, int ldx,
                                                         const float* __restrict__ w, int S, int seg,
                                                         float* __restrict__ p1, unsigned char* __restrict__ arg1,
