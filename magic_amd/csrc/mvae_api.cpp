@@ -500,7 +500,10 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     const int B2 = 2 * (int)B;
     T.nchunk1 = std::min(B2, 1024);
     T.nchunk2 = std::min(B2, 32);
-    T.nchunk2m = std::min(B2, 128);
+    // image chunks of the MFMA weight gradient: 64 -> 256 workgroups at C5CONV, one per CU
+    // (same box: 1.085 ms vs 1.11 at 128 and 1.17 at 256, profiles/r2/conv2_wgrad_ab.txt)
+    T.nchunk2m = std::min(B2, 64);
+    if (const char* nc = std::getenv("MVAE_CONV2_NCHUNK"); nc && std::atoi(nc) > 0) T.nchunk2m = std::min(B2, std::atoi(nc));
     const size_t s1 = (size_t)2 * T.nchunk1 * 26 * 64;
     const size_t s2 = (size_t)2 * (T.mfma ? T.nchunk2m : T.nchunk2) * (25 * 64 + 1) * 64;
     ALLOC(T.slab, std::max(s1, s2));
@@ -1419,7 +1422,7 @@ extern "C" int mvae_debug_conv2(int S1, int B, int mode, int mfma, const float* 
   const size_t img = (size_t)S1 * S1 * 64;
   const int B2 = 2 * B;
   T.nchunk2 = std::min(B2, 32);
-  T.nchunk2m = std::min(B2, 128);
+  T.nchunk2m = std::min(B2, 64);
   std::vector<void*> tmp;
   hipError_t e = hipSuccess;
   auto alloc = [&](size_t bytes) -> void* {
