@@ -220,10 +220,10 @@ __device__ __attribute__((aligned(16))) int4 g_zero16[1];
 typedef __attribute__((address_space(3))) short lds_short;
 
 // operand image of one k-tile (BK = 64 or 32) of ROWS (256 or 128) rows: NG DMA instructions
-// per thread (512 threads x 16 B each)
-template <bool KC, int BK, int ROWS = 256>
+// per thread (NW waves x 64 lanes x 16 B each)
+template <bool KC, int BK, int ROWS = 256, int NW = 8>
 struct WLoad {
-  static constexpr int NG = ROWS * BK / 4096;
+  static constexpr int NG = ROWS * BK / (NW * 512);
   static constexpr int CPR = BK / 8;    // 16-B chunks per row of a k-contiguous image
   static constexpr int RPB = 128 / BK;  // k-contiguous rows per 256-B bank row
   static constexpr int CPK = ROWS / 8;  // 16-B chunks per k-row of a row-contiguous image
@@ -234,7 +234,7 @@ struct WLoad {
   __device__ __forceinline__ void init(int ld, int r0, int nrows, int wave, int lane) {
 #pragma unroll
     for (int j = 0; j < NG; ++j) {
-      const int q = (j * 8 + wave) * 64 + lane;  // chunk this lane copies
+      const int q = (j * NW + wave) * 64 + lane;  // chunk this lane copies
       if constexpr (KC) {
         const int row = q / CPR;
         const int c = (q % CPR) ^ swz(row);
@@ -260,7 +260,7 @@ struct WLoad {
       const bool ok = rv[j] && k0 + kc[j] < kend;
       const unsigned short* src = KC ? g + off[j] + k0 : g + off[j] + (long long)k0 * ld;
       src = ok ? src : reinterpret_cast<const unsigned short*>(g_zero16);
-      __builtin_amdgcn_global_load_lds(src, (lds_short*)(img + (j * 8 + wave) * 512), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(src, (lds_short*)(img + (j * NW + wave) * 512), 16, 0, 0);
     }
   }
   // LDS instructions per fragment
@@ -724,7 +724,7 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (TE) epilogue_wide<EPI, NI>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag);
+  if constexpr (TE) epilogue_rm<EPI, 4, NI, 4, WNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag);
   else epilogue_g<EPI, 4, NI, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
 }
 
@@ -746,6 +746,120 @@ hipError_t launch_q_l(const PParams& p, bool at, bool bt, hipStream_t st) {
 template <int EPI, bool TE>
 hipError_t launch_q_t(const PParams& p, bool at, bool bt, hipStream_t st) {
   return p.g.tn == 128 ? launch_q_l<EPI, TE, 128>(p, at, bt, st) : launch_q_l<EPI, TE, 256>(p, at, bt, st);
+}
+
+// ---------------------------------------------------------------------------------------
+// Twin kernel: 128x128x64 tile, 256 threads = 4 waves (2x2), each wave 64x64 = 2x2 MFMA
+// 32x32x16 accumulators; operand images HBM -> LDS by global_load_lds_dwordx4 (the wide
+// kernels' swizzled lane-linear images at 128 rows) into two stages of 2 x 16 KB. 64 KB of LDS
+// and <= 256 VGPRs, so TWO workgroups share a CU: one's epilogue (activation / BCE math, the
+// LDS transpose and 16-B row stores of the fp32 output and bf16 planes) and its prologue DMA
+// latency run beside the other's k-loop. For the GEMMs whose K is short or whose N ~ 500
+// (hidden encoder layers, the 500-wide dgrads, the BCE decoder output): on the one-workgroup
+// 256-row kernels each tile's epilogue and prologue are exposed, and 500-wide outputs give too
+// few 256x256 tiles to fill 256 CUs without split-K slabs.
+// Pipeline: one barrier per k-tile; the copy of iteration it+1 is issued right after it, into
+// the stage iteration it-1 read, and waited for (vmcnt(0)) at the top of it+1.
+constexpr int TT = 128, TNT = 256;
+
+template <bool AT, bool BT, int EPI, bool TE>
+__global__ __launch_bounds__(TNT, 2) void gemm_bf16t_kernel(PParams pp) {
+  constexpr int BK = 64;
+  constexpr int IMG = TT * BK;  // bf16 elements per operand image
+  const Params& p = pp.g;
+  if (epi_skip<EPI>(p.epi)) return;
+  __shared__ __attribute__((aligned(16))) short smem[2 * 2 * IMG];  // [stage][A | B] = 64 KB
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const Tile t = tile_of_t<TT, TT>(p, true);
+  const unsigned short* __restrict__ A = pp.A + t.bi * p.sA;
+  const unsigned short* __restrict__ Bm = pp.B + t.bi * p.sB;
+
+  WLoad<!AT, BK, TT, 4> la;
+  WLoad<BT, BK, TT, 4> lb;
+  la.init(p.lda, t.m0, p.M, wave, lane);
+  lb.init(p.ldb, t.n0, p.N, wave, lane);
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int np = (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
+  const int nkt = t.ks < t.ke ? (t.ke - t.ks + BK - 1) / BK : 0;
+  const int total = np * nkt;
+  int ipr = 0, ikt = 0;  // (pair, k-tile) of the next copy
+  auto issue = [&](int stage) {
+    short* img = smem + stage * 2 * IMG;
+    const int k0 = t.ks + ikt * BK;
+    const int pab = pp.pab >> (4 * ipr);
+    la.issue(A + (pab & 3) * pp.pA, p.lda, k0, t.ke, img, wave);
+    lb.issue(Bm + ((pab >> 2) & 3) * pp.pB, p.ldb, k0, t.ke, img + IMG, wave);
+    if (++ikt == nkt) { ikt = 0; ++ipr; }
+  };
+  constexpr int NRD = 2 * WLoad<!AT, BK, TT, 4>::NRD + 2 * WLoad<BT, BK, TT, 4>::NRD;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
+  if (total > 0) issue(0);
+  for (int it = 0; it < total; ++it) {
+    const int stage = it & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();  // tile it landed for every wave; stage it-1 no longer read
+    asm volatile("" ::: "memory");
+    if (it + 1 < total) issue(stage ^ 1);
+    const short* sa = smem + stage * 2 * IMG;
+    const short* sb = sa + IMG;
+    const unsigned la0 = lds0 + 2u * (unsigned)(stage * 2 * IMG);
+    const unsigned lb0 = la0 + 2u * IMG;
+    bf16x8 fa[2][2], fb[2][2];
+    auto rd = [&](int ks, bf16x8 (&a)[2], bf16x8 (&b)[2]) {
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) b[ni] = lb.frag(sb, lb0, wn * 64 + ni * 32, ks, lane);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) a[mi] = la.frag(sa, la0, wm * 64 + mi * 32, ks, lane);
+    };
+    rd(0, fa[0], fb[0]);
+#pragma unroll
+    for (int ks = 0; ks < BK / 16; ++ks) {
+      if (ks + 1 < BK / 16) {
+        rd(ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
+        wait_lds<NRD>();
+      } else {
+        wait_lds<0>();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks & 1][mi], fb[ks & 1][ni],
+                                                                acc[mi][ni], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (TE) epilogue_rm<EPI, 2, 2, 2, TNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag);
+  else epilogue_g<EPI, 2, 2, TT, 2>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
+}
+
+template <bool AT, bool BT, int EPI, bool TE>
+hipError_t launch_tw(const PParams& p, hipStream_t st) {
+  const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
+  hipLaunchKernelGGL((gemm_bf16t_kernel<AT, BT, EPI, TE>), dim3(nwg), dim3(TNT), 0, st, p);
+  return hipGetLastError();
+}
+
+template <int EPI, bool TE>
+hipError_t launch_twin_l(const PParams& p, bool at, bool bt, hipStream_t st) {
+  if (!at && !bt) return launch_tw<false, false, EPI, TE>(p, st);
+  if (at && !bt) return launch_tw<true, false, EPI, TE>(p, st);
+  if (!at && bt) return launch_tw<false, true, EPI, TE>(p, st);
+  return launch_tw<true, true, EPI, TE>(p, st);
 }
 
 template <bool AT, bool BT, int EPI, bool SP>
@@ -799,6 +913,13 @@ bool wide_epi_vec_ok(const Params& g) {
 // otherwise (0, 3) the interleaved ring form
 template <int EPI>
 hipError_t launch_wide(const PParams& p, bool at, bool bt, int variant, hipStream_t st) {
+  constexpr bool BCE = EPI == EPI_BCE || EPI == EPI_BCEB;
+  if (p.g.tn == TN_TWIN) {
+    // row-major epilogue through LDS where the tile writes bf16 planes or is the BCE head
+    // (variant 14: also for fp32-only outputs)
+    const bool te = (p.g.epi.cp || BCE || variant == 14) && wide_epi_vec_ok(p.g);
+    return te ? launch_twin_l<EPI, true>(p, at, bt, st) : launch_twin_l<EPI, false>(p, at, bt, st);
+  }
   if constexpr (EPI == EPI_STORE) {
     if (variant == 5) return launch_wide_t<EPI, 32, 4>(p, at, bt, st);
     if (variant == 7) return launch_ring_t<EPI, true>(p, at, bt, st);
@@ -811,7 +932,6 @@ hipError_t launch_wide(const PParams& p, bool at, bool bt, int variant, hipStrea
   // when the tile writes bf16 planes or is the BCE head (2-B plane stores and 4-B target loads
   // per element otherwise), and stays in the C/D layout for fp32-only outputs (split-K slabs:
   // 128-B row segments already, where the LDS round trip measured 5-10 % slower)
-  constexpr bool BCE = EPI == EPI_BCE || EPI == EPI_BCEB;
   if ((p.g.epi.cp || BCE) && variant != 10 && wide_epi_vec_ok(p.g))
     return launch_q_t<EPI, true>(p, at, bt, st);
   return launch_q_t<EPI, false>(p, at, bt, st);
@@ -849,9 +969,10 @@ hipError_t launch_var(const PParams& p, bool at, bool bt, int variant, hipStream
 
 bool gemm_bf16_wide(const GemmDesc& d) {
   if (d.prec == GEMM_F32) return false;
-  // 10-12: default-shape variants of the interleaved kernel (old epilogue, forced tile N)
-  const int v = d.variant >= 10 ? 0 : d.variant;
-  if (v == 1 || v == 2 || v == 4) return false;  // 128x128 variants
+  // 10-12, 15: default-shape variants of the interleaved kernel (old epilogue, forced tile N,
+  // no twin); 13 / 14: the twin kernel (any shape)
+  const int v = (d.variant >= 10 && d.variant != 13 && d.variant != 14) ? 0 : d.variant;
+  if (v == 1 || v == 2 || v == 4) return false;  // 128x128 register-staged variants
   if (v != 3 && v < 5 && (d.M < 256 || d.N < 256)) return false;
   // one k-tile and under a CU's worth of 256x256 tiles (dec layer 1: K = L + 1; the head's
   // dgrad: K = 2L): epilogue-bound on few CUs, the 128x128 kernels spread it wider
@@ -864,10 +985,13 @@ bool gemm_bf16_wide(const GemmDesc& d) {
   return true;
 }
 
-// Joint choice of the tile N (256 or 128) and split-K for the wide kernel: one 256 x TN x 64
-// k-tile per CU per iteration (one workgroup per CU) + prologue/epilogue; split-K adds the fp32
-// slab round trip and the reduction launch. Variants 11 / 12 force TN 128 / 256.
-static void wide_plan(const GemmDesc& d, size_t max_ws, int* split, int* tn) {
+// Joint choice of the kernel (256 x 256 / 256 x 128 one-workgroup-per-CU ring kernels, or the
+// 128 x 128 twin kernel at two workgroups per CU) and split-K: each kernel's time is its rounds
+// of resident workgroups x (k-tiles + fixed prologue/epilogue cost) x its time per k-tile;
+// split-K adds the fp32 slab round trip and the reduction launch. Variants 11 / 12 force the
+// ring kernel at tile N 128 / 256, 13 / 14 the twin kernel, 15 the ring kernels only.
+struct WidePlan { int split = 1; int tn = 256; };
+static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
   const bool fixed = d.epi.mode == EPI_BCE || d.epi.mode == EPI_BCEB || d.epi.mode == EPI_SIGMOID;
   const int kt = (d.K + 63) / 64;
   const int T = d.nA > d.nB ? d.nA : d.nB;
@@ -875,39 +999,40 @@ static void wide_plan(const GemmDesc& d, size_t max_ws, int* split, int* tn) {
   for (int i = 0; i < d.nA; ++i)
     for (int j = 0; j < d.nB; ++j) np += i + j < T;
   if (d.dynA) np = (np + (d.nB < T ? d.nB : T)) / 2;  // A's residual planes often all zero
+  const bool big = d.M >= 256 && d.N >= 256;
   double best = 1e30;
-  *split = 1;
-  *tn = 256;
-  for (int w : {256, 128}) {
+  WidePlan pl;
+  for (int w : {256, 128, TN_TWIN}) {
+    const bool twin = w == TN_TWIN;
     if (d.variant == 11 && w != 128) continue;
     if (d.variant == 12 && w != 256) continue;
-    const long long tiles = (long long)((d.M + WT - 1) / WT) * ((d.N + w - 1) / w) * d.batch;
-    // measured: 4096^3 at 1.06 PF/s = 1.94 us per 256x256 k-tile per CU; the 256x128 tile does
-    // half the MFMA work per k-tile in ~1.5 us (profiles/r2/gemm_ab_tile_n.txt: it wins only
-    // where it removes a split-K reduction, e.g. the encoder dgrads and the 500-wide decoder)
-    const double t_kt = w == 256 ? 1.9e-6 : 1.5e-6;
+    if ((d.variant == 13 || d.variant == 14) && !twin) continue;
+    if (d.variant == 15 && twin) continue;
+    if (!twin && !big && d.variant != 3 && d.variant < 5) continue;
+    const int tm = twin ? TT : WT, tnn = twin ? TT : w;
+    const long long tiles = (long long)((d.M + tm - 1) / tm) * ((d.N + tnn - 1) / tnn) * d.batch;
+    // ring kernels, measured: 4096^3 at 1.06 PF/s = 1.94 us per 256x256 k-tile per CU; the
+    // 256x128 tile does half the MFMA work per k-tile in ~1.5 us (profiles/r2/gemm_ab_tile_n.txt).
+    // twin: two resident 128x128 workgroups per CU, t_kt per k-tile of one of them, epilogue
+    // and prologue mostly hidden behind the co-resident workgroup
+    const double t_kt = twin ? 0.55e-6 : (w == 256 ? 1.9e-6 : 1.5e-6);
+    const double slots = twin ? 512.0 : 256.0;
+    const double fix = twin ? 1.5 : 3.0;
     for (int s = 1; s <= (fixed ? 1 : 32); ++s) {
       if (s > 1 && kt / s < 2) break;
       if (s > 1 && (size_t)d.batch * s * d.M * d.N > max_ws) break;
-      const double rounds = std::ceil(tiles * s / 256.0);
-      double t = rounds * (np * std::ceil((double)kt / s) + 3.0) * t_kt;
+      const double rounds = std::ceil(tiles * s / slots);
+      double t = rounds * (np * std::ceil((double)kt / s) + fix) * t_kt * (twin ? 2.0 : 1.0);
       if (s > 1) t += (double)d.batch * s * d.M * d.N * 8.0 / 4.5e12 + 4e-6;
-      if (t < best * 0.97) { best = t; *split = s; *tn = w; }
+      if (t < best * 0.97) { best = t; pl.split = s; pl.tn = w; }
     }
   }
+  return pl;
 }
 
-int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws) {
-  int s, tn;
-  wide_plan(d, max_ws, &s, &tn);
-  return s;
-}
+int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws) { return wide_plan(d, max_ws).split; }
 
-int gemm_bf16_wide_tn(const GemmDesc& d, size_t max_ws) {
-  int s, tn;
-  wide_plan(d, max_ws, &s, &tn);
-  return tn;
-}
+int gemm_bf16_wide_tn(const GemmDesc& d, size_t max_ws) { return wide_plan(d, max_ws).tn; }
 
 hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, hipStream_t st) {
   PParams p;
@@ -929,11 +1054,11 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   for (int i = 0; i < n; ++i) p.pab |= (p.pa[i] | p.pb[i] << 2) << (4 * i);
   if (gemm_bf16_wide(d)) {
     // tile N: the planner's (gemm_run), 256 for the diagnostic variants of the 256x256 forms
-    const bool q = d.variant == 0 || d.variant == 3 || d.variant == 10 || d.variant == 11 ||
-                   d.variant == 12;
-    p.g.tn = q && g.tn == 128 ? 128 : 256;
-    p.g.ntm = (d.M + WT - 1) / WT;
-    p.g.ntn = (d.N + p.g.tn - 1) / p.g.tn;
+    const bool q = d.variant == 0 || d.variant == 3 || (d.variant >= 10 && d.variant <= 15);
+    p.g.tn = q && (g.tn == 128 || g.tn == TN_TWIN) ? g.tn : 256;
+    const int tm = p.g.tn == TN_TWIN ? TT : WT, tn = p.g.tn == TN_TWIN ? TT : p.g.tn;
+    p.g.ntm = (d.M + tm - 1) / tm;
+    p.g.ntn = (d.N + tn - 1) / tn;
     switch (epi) {
       case EPI_STORE: return launch_wide<EPI_STORE>(p, d.at, d.bt, d.variant, st);
       case EPI_ACT: return launch_wide<EPI_ACT>(p, d.at, d.bt, d.variant, st);

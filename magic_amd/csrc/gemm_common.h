@@ -20,9 +20,10 @@ struct Params {
   long long sA, sB, sC;     // batch strides
   int batch, split, kchunk;
   int ntm, ntn;
-  int tn;                   // wide bf16 kernel: tile N (256 or 128)
+  int tn;                   // bf16 DMA kernels: ring-kernel tile N (256 or 128) or TN_TWIN
   GemmEpi epi;
 };
+constexpr int TN_TWIN = 1;  // Params::tn of the 128 x 128 twin kernel (gemm_bf16.hip)
 
 __device__ __forceinline__ float act_f(float v, int act) {
   if (act == ACT_TANH) return tanhf(v);
@@ -241,13 +242,17 @@ __device__ __forceinline__ void st8_planes(unsigned short* cp, long long pc, int
 }
 
 // diag (timing diagnostics, results meaningless): bit 1 = no global stores, bit 2 = no LDS
-// transpose, bit 3 = no transcendental math. Tile 256 x 128*NI (waves 2 x 4, acc [4][NI]).
-template <int EPI, int NI>
-__device__ __forceinline__ void epilogue_wide(const Params& p, const Tile& t, f32x16 (&acc)[4][NI],
-                                              float* lds, int wm, int wn, int diag = 0) {
-  constexpr int TW = 128 * NI, BAND = 64 * TW;  // band row width, floats per band buffer
+// transpose, bit 3 = no transcendental math. Waves 2 (M) x NWN (N), NTH threads, each wave
+// acc[MI][NI] 32x32 blocks: tile (64*MI) x TW, TW = NWN*NI*32 (a multiple of 128). Band mi =
+// accumulator row block mi of both wave rows (64 rows); `lds` holds two bands (2 x 64 x TW fp32).
+// Wide kernels: MI 4, NWN 4, NTH 512 (256 x 128*NI tiles); twin kernel: 2, 2, 2, 256 (128 x 128).
+template <int EPI, int MI, int NI, int NWN, int NTH>
+__device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x16 (&acc)[MI][NI],
+                                            float* lds, int wm, int wn, int diag = 0) {
+  constexpr int TW = NWN * NI * 32, BAND = 64 * TW;  // band row width, floats per band buffer
+  static_assert(TW % 128 == 0, "BCE row partials are per 128-column block");
   constexpr int CW = TW / 8;                    // 8-column chunks per band row
-  constexpr int RP = 512 / CW;                  // band rows per reader pass
+  constexpr int RP = NTH / CW;                  // band rows per reader pass
   constexpr bool BCE = EPI == EPI_BCE || EPI == EPI_BCEB;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -257,9 +262,9 @@ __device__ __forceinline__ void epilogue_wide(const Params& p, const Tile& t, f3
   const int c8 = tid % CW, rr = tid / CW;   // reader: chunk of 8 columns, row within RP
   const int col0 = t.n0 + 8 * c8;
   const int nblk = (p.N + 127) / 128;
-  const int gb = t.nt * NI + (c8 >> 4);     // 128-column block of this chunk
+  const int gb = t.nt * (TW / 128) + (c8 >> 4);  // 128-column block of this chunk
 #pragma unroll
-  for (int mi = 0; mi < 4; ++mi) {
+  for (int mi = 0; mi < MI; ++mi) {
     float* band = lds + (mi & 1) * BAND;
     // writer: this wave's 32 x (TW/4) block of the band, C/D layout -> row-major
     if (!(diag & 4))
@@ -268,13 +273,13 @@ __device__ __forceinline__ void epilogue_wide(const Params& p, const Tile& t, f3
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        band[row * TW + wn * (TW / 4) + ni * 32 + (lane & 31)] = acc[mi][ni][r];
+        band[row * TW + wn * (NI * 32) + ni * 32 + (lane & 31)] = acc[mi][ni][r];
       }
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < 64 / RP; ++q) {
       const int br = rr + RP * q;                                    // band row
-      const int row = t.m0 + (br >> 5) * 128 + mi * 32 + (br & 31);  // tile row -> global
+      const int row = t.m0 + (br >> 5) * (MI * 32) + mi * 32 + (br & 31);  // tile row -> global
       float v[8];
       const float4 a = *reinterpret_cast<const float4*>(band + br * TW + 8 * c8);
       const float4 b = *reinterpret_cast<const float4*>(band + br * TW + 8 * c8 + 4);

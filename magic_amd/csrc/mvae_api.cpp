@@ -523,6 +523,10 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   }
   build_schedule(c);
   if (const char* nv = std::getenv("MVAE_NO_VALU"); nv && *nv == '1') c->valu = false;
+  // kernel A/B switch (diagnostics): MVAE_TWIN=0 plans the bf16 DMA GEMMs on the ring kernels
+  // only (round-2 plan), 2 forces the 128x128 twin kernel wherever a ring kernel would run
+  int twin_mode = 1;
+  if (const char* tw = std::getenv("MVAE_TWIN"); tw && (*tw == '0' || *tw == '2')) twin_mode = *tw - '0';
   const int gp = cfg->precision == MVAE_PREC_BF16 ? GEMM_BF16
                  : (cfg->precision == MVAE_PREC_F32X ? GEMM_F32X : GEMM_F32);
   c->np = gp == GEMM_BF16 ? 1 : (gp == GEMM_F32X ? 3 : 0);
@@ -579,6 +583,8 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     // latent head, thin decoder layers) run faster as one native fp32 MFMA GEMM than as six
     // bf16 plane products on the 128x128 kernel; same accuracy class
     if (gp == GEMM_F32X && !gemm_bf16_wide(d)) d.prec = GEMM_F32;
+    if (d.prec != GEMM_F32 && !d.valu && gemm_bf16_wide(d) && twin_mode != 1)
+      d.variant = twin_mode == 0 ? 15 : 13;
   };
   for (auto* v : {&c->fwd_enc, &c->bwd_dec, &c->bwd_enc})
     for (auto& d : *v) wire(d);
@@ -656,9 +662,10 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     // the GEMM plans of this context (diagnostics): shape, arithmetic, kernel, split-K + combine
     auto show = [&](const GemmDesc& d, int r) {
       const int sp = gemm_plan_split(d, ws);
-      std::fprintf(stderr, "[mvae plan] %-16s M %6d N %6d K %6d batch %d prec %d wide %d split %d\n",
-                   r >= 0 ? c->region_names[r].c_str() : "?", d.M, d.N, d.K, d.batch, d.prec,
-                   (int)gemm_bf16_wide(d), sp);
+      const bool wide = gemm_bf16_wide(d);
+      std::fprintf(stderr, "[mvae plan] %-16s M %6d N %6d K %6d batch %d prec %d valu %d wide %d tile_n %d split %d\n",
+                   r >= 0 ? c->region_names[r].c_str() : "?", d.M, d.N, d.K, d.batch, d.prec, d.valu,
+                   (int)wide, wide ? gemm_bf16_wide_tn(d, ws) : 0, sp);
     };
     for (size_t i = 0; i < c->fwd_enc.size(); ++i) show(c->fwd_enc[i], c->fwd_enc_r[i]);
     show(c->f_d1, c->f_d1_r); show(c->f_d2, c->f_d2_r); show(c->f_out, c->f_out_r);
@@ -1320,10 +1327,11 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   // operand rows padded to 8 elements (16 B), as the step's buffers are
   const int lda = ((at ? M : K) + 7) & ~7, ldb = ((bt ? K : N) + 7) & ~7;
   const size_t sa = (size_t)(at ? K : M) * lda, sb = (size_t)(bt ? N : K) * ldb;
-  const size_t na = sa * batch, nb = sb * batch, nc = (size_t)M * N * batch;
+  const int ldc = (N + 7) & ~7;  // output rows padded to 16 B as well (the 16-B epilogue stores)
+  const size_t na = sa * batch, nb = sb * batch, nc = (size_t)M * ldc * batch;
   float *A = nullptr, *Bm = nullptr, *Cm = nullptr, *ws = nullptr;
-  GemmDesc d = gd(M, N, K, nullptr, lda, at != 0, nullptr, ldb, bt != 0, nullptr, N);
-  d.batch = batch; d.sA = (long long)sa; d.sB = (long long)sb; d.sC = (long long)M * N;
+  GemmDesc d = gd(M, N, K, nullptr, lda, at != 0, nullptr, ldb, bt != 0, nullptr, ldc);
+  d.batch = batch; d.sA = (long long)sa; d.sB = (long long)sb; d.sC = (long long)M * ldc;
   d.variant = variant & 15;
   d.prec = (variant >> 4) & 15;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
   if (d.variant == 9) { d.valu = 1; d.prec = GEMM_F32; d.variant = 0; }  // the fp32 VALU kernel
@@ -1353,11 +1361,11 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
     if (epi > EPI_SIGMOID) e = hipErrorInvalidValue;
     d.epi.mode = epi;
     d.epi.act = ACT_TANH;
-    if (e == hipSuccess) e = hipMalloc(&aux, (size_t)M * N * 4);
-    if (e == hipSuccess) e = launch_normal(aux, 1, 1, M * N, 1, 0, 3, 0, st);
+    if (e == hipSuccess) e = hipMalloc(&aux, (size_t)M * ldc * 4);
+    if (e == hipSuccess) e = launch_normal(aux, 1, 1, M * ldc, 1, 0, 3, 0, st);
     if (e == hipSuccess && epi == EPI_BCE) e = hipMalloc(&rowpart, (size_t)M * gemm_bce_nblk(N) * 4);
-    d.epi.aux = aux; d.epi.ld_aux = N;
-    d.epi.x = aux; d.epi.ldx = N;
+    d.epi.aux = aux; d.epi.ld_aux = ldc;
+    d.epi.x = aux; d.epi.ldx = ldc;
     d.epi.rowpart = rowpart;
     d.epi.scale = 1.f / M;
     if (e == hipSuccess && np) {

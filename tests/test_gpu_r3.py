@@ -1,0 +1,115 @@
+"""GPU parity for the round-3 items: the 128x128 twin GEMM kernel (two workgroups per CU) on
+every operand layout, ragged edge and fused epilogue, and whole training steps with the twin
+kernel forced onto every bf16 DMA GEMM (MVAE_TWIN=2) or excluded (MVAE_TWIN=0), against the
+float64 oracle at the fp32 bar (f32x) and the documented bf16 bar."""
+import pytest
+import torch
+
+from magic_amd import _lib
+from magic_amd.config import baseline_config, preset
+from tests.test_gpu_parity import _padded, check_step
+
+pytestmark = pytest.mark.gpu
+
+BF16 = dict(tol=5e-2, loss_tol=2e-3, dist_tol=2e-2)  # documented bf16 tolerance
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+# ------------------------------------------------------------------ twin kernel
+@pytest.mark.parametrize("prec", [2, 1], ids=["f32x", "bf16"])
+@pytest.mark.parametrize("at,bt", [(0, 0), (1, 0), (0, 1), (1, 1)])
+@pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 13), (300, 517, 1001, 13), (1000, 600, 4099, 13),
+                                           (513, 260, 130, 14), (40, 70, 200, 13), (2100, 500, 700, 14),
+                                           (129, 40, 8193, 13), (1, 8, 1, 13)])
+def test_gemm_twin_kernel(at, bt, M, N, K, variant, prec):
+    """Variant 13 / 14 force the twin kernel (14 also routes fp32-only outputs through its LDS
+    row-major epilogue); ragged M / N / K edges and the planner's split-K (K 4099, 8193)."""
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(M * 5 + N * 11 + K + variant)
+    A = _padded(K, M, g) if at else _padded(M, K, g)
+    Bm = _padded(N, K, g) if bt else _padded(K, N, g)
+    C = torch.full((M, N), float("nan"), device="cuda")
+    rc = lib.mvae_debug_gemm(M, N, K, A.data_ptr(), A.shape[1], at, Bm.data_ptr(), Bm.shape[1], bt,
+                             C.data_ptr(), N, (prec << 4) | (variant << 8), 0, None, 0,
+                             torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, lib.mvae_last_error(None)
+    Ad = (A[:, :M].double().T if at else A[:, :K].double())
+    Bd = (Bm[:, :K].double().T if bt else Bm[:, :N].double())
+    ref = Ad @ Bd
+    err = (C.double() - ref).abs().max().item()
+    mag = (Ad.abs() @ Bd.abs()).max().item()
+    bound = (2e-6 if prec != 1 else 1e-2) * mag + 1e-6
+    assert err <= bound, (err, bound)
+
+
+@pytest.mark.parametrize("prec", [2, 1], ids=["f32x", "bf16"])
+@pytest.mark.parametrize("epi,act", [(1, 0), (1, 1), (2, 0), (2, 1), (4, 0)])
+@pytest.mark.parametrize("M,N,ldc", [(600, 520, 520), (300, 500, 500), (130, 257, 264), (280, 300, 301)])
+@pytest.mark.parametrize("variant,planes", [(13, 0), (13, 1), (14, 0)])
+def test_gemm_twin_epilogues(prec, epi, act, M, N, ldc, variant, planes):
+    """Fused ACT / DACT / SIGMOID epilogues of the twin kernel against float64, in both its
+    epilogue forms (C/D layout; LDS row-major with 16-B stores and element tails, ld 301 falls
+    back to the C/D layout); nothing written past column N."""
+    lib = _lib.load()
+    K = 304
+    g = torch.Generator(device="cuda").manual_seed(M + 7 * N + 31 * epi + act + variant)
+    A = torch.randn(M, K, device="cuda", generator=g) * 0.3
+    Bm = _padded(K, N, g) * 0.3
+    ld_aux = (N + 7) // 8 * 8
+    pre = torch.randn(M, ld_aux, device="cuda", generator=g)
+    aux = torch.tanh(pre) if act == 0 else torch.nn.functional.elu(pre)
+    C = torch.full((M, ldc), float("nan"), device="cuda")
+    rc = lib.mvae_debug_gemm(M, N, K, A.data_ptr(), K, 0, Bm.data_ptr(), Bm.shape[1], 0, C.data_ptr(),
+                             ldc, epi | (prec << 4) | (variant << 8) | (planes << 12), act,
+                             aux.data_ptr(), ld_aux, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, lib.mvae_last_error(None)
+    acc = A.double() @ Bm[:, :N].double()
+    a = aux[:, :N].double()
+    if epi == 1:
+        ref = torch.tanh(acc) if act == 0 else torch.where(acc < 0, torch.exp(acc) - 1, acc)
+    elif epi == 2:
+        ref = acc * (1 - a * a) if act == 0 else torch.where(a < 0, acc * (a + 1), acc)
+    else:
+        ref = torch.sigmoid(acc)
+    mag = (A.double().abs() @ Bm[:, :N].double().abs()).max().item()
+    bound = (2e-6 if prec == 2 else 1e-2) * mag + 1e-6
+    if planes and prec == 1:  # one RN bf16 plane of the output
+        bound += 2.0 ** -8 * ref.abs().max().item()
+    err = (C[:, :N].double() - ref).abs().max().item()
+    assert err <= bound, (err, bound)
+    if ldc > N and not planes:
+        assert torch.isnan(C[:, N:]).all()
+
+
+@pytest.mark.parametrize("mode", ["0", "2"], ids=["ring_only", "twin_everywhere"])
+@pytest.mark.parametrize("prec", ["f32x", "bf16"])
+@pytest.mark.parametrize("grey", [False, True], ids=["binary", "grey"])
+def test_step_twin_modes(monkeypatch, mode, prec, grey):
+    """A whole step with every bf16 DMA GEMM on the twin kernel (BCE head with fp32 or bf16-plane
+    target, DACT row remap, batch-2 weight gradients, split-K) or on the ring kernels only."""
+    monkeypatch.setenv("MVAE_TWIN", mode)
+    cfg = preset("8c", image_size=20, batch=288, precision=prec).replace(enc=(300, 260, 280))
+    if prec == "f32x":
+        check_step(cfg, grey=grey, recon=True)
+    else:
+        check_step(cfg, grey=grey, recon=True, **BF16)
+
+
+@pytest.mark.parametrize("mode", ["1", "2"], ids=["planner", "twin_everywhere"])
+def test_step_c3_shape_twin(monkeypatch, mode):
+    """BASELINE C3's shapes (8d, bf16, 100x100, enc [500]*4, L = 200) at B = 2048 with the default
+    plan and with the twin kernel everywhere, documented bf16 bar."""
+    monkeypatch.setenv("MVAE_TWIN", mode)
+    check_step(baseline_config("C3").replace(batch=2048), adam=False, **BF16)
+
+
+def test_step_c2_f32x_twin_everywhere(monkeypatch):
+    """The benched C2 configuration (f32x, B = 4096) with the twin kernel on every bf16 GEMM, at the
+    fp32 bar."""
+    monkeypatch.setenv("MVAE_TWIN", "2")
+    check_step(preset("8c", image_size=100, batch=4096, precision="f32x"), adam=False)
