@@ -353,6 +353,10 @@ def cpu_baseline(cfg, dev, seconds: float):
         return n * X.shape[0] / dt, n, dt
     blas = [i for i in threadpool_info() if i.get("user_api") == "blas"]
     cores = max([i.get("num_threads", 1) for i in blas] or [1])
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count()
     v_c1, n_c1, t_c1 = timed(X1, A1, E1, seconds)
     with threadpool_limits(1):
         v_c1_1, n_c1_1, t_c1_1 = timed(X1, A1, E1, seconds)
@@ -370,6 +374,11 @@ def cpu_baseline(cfg, dev, seconds: float):
             "c1_all_threads": round(v_c1, 2), "c1_one_thread": round(v_c1_1, 2),
             "c1_sample": f"{n_c1} / {n_c1_1} steps x {B1} pairs ({t_c1:.1f} / {t_c1_1:.1f} s)",
             "cpu_model": _cpu_model(), "os_cpu_count": os.cpu_count(),
+            "affinity_cpus": affinity, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "threads_note": (f"all-thread legs use the BLAS pool's {cores} threads: OMP_NUM_THREADS="
+                             f"{os.environ.get('OMP_NUM_THREADS')} is this lease's CPU share (a one-GPU "
+                             f"slice of the host; the process may run on {affinity} of the host's "
+                             f"{os.cpu_count()} CPUs, which other leases share)"),
             "torch_threads": torch.get_num_threads(),
             "parity_c1": {"gpu_precision": cfg.precision, "bar": bar, **{k: float(f"{v:.3g}") for k, v in parity.items()},
                           "ok": all(v <= bar for v in parity.values()),

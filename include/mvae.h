@@ -110,6 +110,10 @@ enum {
 };
 
 int mvae_abi_version(void);
+/* Build id: the first 16 hex digits of the SHA-256 of the library's sources (magic_amd/csrc/*
+ * and this header) at compile time (magic_amd/build.py source_hash). The Python loader refuses
+ * a library whose id differs from the sources on disk, so a stale libmvae.so fails loudly. */
+const char* mvae_build_id(void);
 int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out);
 int mvae_destroy(mvae_ctx* ctx);
 const char* mvae_last_error(mvae_ctx* ctx);   /* ctx may be NULL (creation errors) */

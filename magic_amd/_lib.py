@@ -53,6 +53,7 @@ class mvae_tensor(C.Structure):
 
 _SIGS = {
     "mvae_abi_version": ([], C.c_int),
+    "mvae_build_id": ([], C.c_char_p),
     "mvae_create": ([C.POINTER(mvae_cfg), C.c_int, C.POINTER(C.c_void_p)], C.c_int),
     "mvae_destroy": ([C.c_void_p], C.c_int),
     "mvae_last_error": ([C.c_void_p], C.c_char_p),
@@ -127,9 +128,24 @@ def load(path: str | None = None):
     v = lib.mvae_abi_version()
     if v != ABI_VERSION:
         raise MVAELibraryError(f"ABI version mismatch: library {v}, binding {ABI_VERSION}")
+    verify_build(lib)
     if path is None:
         _lib = lib
     return lib
+
+
+def verify_build(lib, expected: str | None = None) -> str:
+    """The library's build id must equal the hash of the sources on disk (magic_amd/build.py
+    source_hash): a libmvae.so built from other sources (stale, or shipped from another tree)
+    is refused. Returns the id."""
+    from .build import source_hash
+    got = lib.mvae_build_id().decode()
+    want = expected if expected is not None else source_hash()
+    if got != want:
+        raise MVAELibraryError(
+            f"libmvae.so build id {got} does not match the sources on disk ({want}): the library "
+            "is stale; rebuild it with `python -m magic_amd.build`")
+    return got
 
 
 def check(lib, ctx, rc):

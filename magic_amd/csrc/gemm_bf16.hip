@@ -810,7 +810,7 @@ __global__ __launch_bounds__(TNT, 2) void gemm_bf16t_kernel(PParams pp) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();  // tile it landed for every wave; stage it-1 no longer read
     asm volatile("" ::: "memory");
-    if (it + 1 < total) issue(stage ^ 1);
+    if (it + 1 < total && !(pp.diag & 1)) issue(stage ^ 1);
     const short* sa = smem + stage * 2 * IMG;
     const short* sb = sa + IMG;
     const unsigned la0 = lds0 + 2u * (unsigned)(stage * 2 * IMG);

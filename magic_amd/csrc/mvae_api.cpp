@@ -112,9 +112,9 @@ struct mvae_ctx {
   int64_t t1 = 0, t2 = 0;
   float b1p[2] = {0, 0}, b2p[2] = {0, 0};
   uint64_t rng_counter = 0;   // training draws (eps == NULL in mvae_forward / train_step)
-  uint64_t rng_eval = 0;
-  int row_off = 0;            // this rank's first row in the global batch (eps sampling)      // inference draws (predict / reconstruct): a separate stream, so
+  uint64_t rng_eval = 0;      // inference draws (predict / reconstruct): a separate stream, so
                               // evaluation never shifts the training noise sequence
+  int row_off = 0;            // this rank's first row in the global batch (eps sampling)
   int phase = 0;  // 0 idle, 1 forward done, 2 metric done, 3 backward done
   std::string err;
 };
@@ -335,8 +335,10 @@ static int validate(const mvae_cfg* cfg) {
       cfg->precision != MVAE_PREC_F32X)
     return fail(nullptr, MVAE_ECONFIG, "bad precision");
   if (cfg->conv != 0 && cfg->conv != 1) return fail(nullptr, MVAE_ECONFIG, "conv must be 0 or 1");
-  if (cfg->conv && (cfg->image_size % 4 != 0 || cfg->image_size > 400))
-    return fail(nullptr, MVAE_ECONFIG, "conv encoder: image_size must be a multiple of 4 (<= 400)");
+  // conv tower: sizes up to BASELINE's 100 x 100 are the tested range (tests/test_gpu_conv.py);
+  // larger images would need > 64 KB of dynamic LDS in the conv2 MFMA kernels, never run
+  if (cfg->conv && (cfg->image_size % 4 != 0 || cfg->image_size > 100))
+    return fail(nullptr, MVAE_ECONFIG, "conv encoder: image_size must be a multiple of 4 (<= 100)");
   const long long D = (long long)cfg->image_size * cfg->image_size;
   if (D * 3 * cfg->batch > (1LL << 31) - 1 || 3LL * cfg->batch * (D + 4) > (1LL << 31) * 8)
     return fail(nullptr, MVAE_ECONFIG, "batch too large for 32-bit row indexing");
@@ -346,6 +348,11 @@ static int validate(const mvae_cfg* cfg) {
 extern "C" {
 
 int mvae_abi_version(void) { return MVAE_ABI_VERSION; }
+
+#ifndef MVAE_BUILD_ID
+#error "MVAE_BUILD_ID must be defined by the build (magic_amd/build.py source_hash)"
+#endif
+const char* mvae_build_id(void) { return MVAE_BUILD_ID; }
 
 const char* mvae_last_error(mvae_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_err.c_str(); }
 
@@ -961,10 +968,12 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
   const bool two = c->use_side && c->side;
   hipStream_t sd = two ? c->side : st;
   auto fork = [&]() -> int { return two ? stream_wait(c, st, sd) : MVAE_OK; };
+  // join whatever the side stream still holds, even if "side_stream" was switched off after
+  // the fork (the pending weight gradients would otherwise race with Adam / the all-reduce)
   auto join = [&]() -> int {
-    if (!two || !c->side_pending) return MVAE_OK;
+    if (!c->side || !c->side_pending) return MVAE_OK;
     c->side_pending = false;
-    return stream_wait(c, sd, st);
+    return stream_wait(c, c->side, st);
   };
   if (part == 0) {
     // bwd_dec: W_out, D_out, W_d2, D_d2, W_d1, D_z
@@ -1055,7 +1064,13 @@ extern "C" int mvae_backward(mvae_ctx* ctx, void* stream) {
 extern "C" int mvae_set_option(mvae_ctx* ctx, const char* name, int value) {
   if (!ctx || !name) return MVAE_EINVAL;
   const std::string k(name);
-  if (k == "side_stream") { ctx->use_side = value != 0; return MVAE_OK; }
+  if (k == "side_stream") {
+    // not while forked weight gradients are still un-joined (mid-backward)
+    if (ctx->side_pending)
+      return fail(ctx, MVAE_ESTATE, "side_stream cannot change while side-stream work is pending");
+    ctx->use_side = value != 0;
+    return MVAE_OK;
+  }
   return fail(ctx, MVAE_EINVAL, "unknown option " + k);
 }
 
@@ -1416,7 +1431,7 @@ extern "C" int mvae_make_batch(const unsigned char* locks, const unsigned char* 
 // y = d a2 (4B). mfma: the bf16 MFMA kernels (operands rounded to bf16) instead of fp32 VALU.
 extern "C" int mvae_debug_conv2(int S1, int B, int mode, int mfma, const float* x, const float* y,
                                 float* out, void* stream) {
-  if (S1 <= 0 || S1 > 200 || B <= 0 || mode < 0 || mode > 2 || !x || !y || !out)
+  if (S1 <= 0 || S1 > 50 || B <= 0 || mode < 0 || mode > 2 || !x || !y || !out)
     return fail(nullptr, MVAE_EINVAL, "mvae_debug_conv2: bad argument");
   hipStream_t st = (hipStream_t)stream;
   ConvTower T;

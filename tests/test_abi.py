@@ -69,3 +69,15 @@ def test_engine_fails_loudly_without_gpu():
 def test_missing_library_is_an_error(tmp_path):
     with pytest.raises(_lib.MVAELibraryError):
         _lib.load(str(tmp_path / "nope.so"))
+
+
+def test_build_id_ties_library_to_sources():
+    """libmvae.so carries the hash of the sources it was built from; the loader refuses a
+    library whose id differs from the sources on disk (a stale or foreign build)."""
+    from magic_amd.build import source_files, source_hash
+    lib = _lib.load()
+    assert lib.mvae_build_id().decode() == source_hash()
+    assert any(p.endswith("mvae_api.cpp") for p in source_files())
+    assert any(p.endswith(os.path.join("include", "mvae.h")) for p in source_files())
+    with pytest.raises(_lib.MVAELibraryError, match="stale"):
+        _lib.verify_build(lib, expected="0" * 16)

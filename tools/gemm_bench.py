@@ -44,29 +44,35 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--epilogues", action="store_true", help="run each shape with its step epilogue")
+    ap.add_argument("--diag", default="0", help="kernel diagnostics bits (PParams::diag), comma list")
+    ap.add_argument("--shapes", default="", help="comma list of shape names (default: all)")
     args = ap.parse_args()
     lib = _lib.load()
     torch.cuda.init()
     st = torch.cuda.current_stream().cuda_stream
     cfg = baseline_config(args.config)
-    variants = [int(v) for v in args.variants.split(",")]
+    variants = [(int(v), int(d)) for v in args.variants.split(",") for d in args.diag.split(",")]
+    want = set(args.shapes.split(",")) if args.shapes else None
+    sh = [s for s in shapes(cfg) if want is None or s[0] in want]
     res = {}
     for _ in range(args.rounds):
-        for name, M, N, K, at, bt, batch, epi in shapes(cfg):
+        for name, M, N, K, at, bt, batch, epi in sh:
             for v in variants:
                 ms = C.c_float()
-                vv = v | (epi << 8 if args.epilogues else 0)
+                vv = v[0] | (epi << 8 if args.epilogues else 0) | (v[1] << 12)
                 rc = lib.mvae_bench_gemm(M, N, K, at, bt, batch, vv, args.iters, st, C.byref(ms))
                 if rc != 0:
                     raise RuntimeError(lib.mvae_last_error(None))
                 res.setdefault((name, v), []).append(ms.value)
-    print(f"{'shape':16s} {'MxNxK':>22s} batch " + " ".join(f"{'v' + str(v) + ' TF/s':>10s}" for v in variants))
-    for name, M, N, K, at, bt, batch, epi in shapes(cfg):
+    lab = [f"v{v}" + (f"d{d}" if d else "") for v, d in variants]
+    print(f"{'shape':16s} {'MxNxK':>22s} batch " + " ".join(f"{x + ' TF/s':>12s}" for x in lab))
+    for name, M, N, K, at, bt, batch, epi in sh:
         fl = 2.0 * M * N * K * batch
         cells = []
         for v in variants:
             med = statistics.median(res[(name, v)])
-            cells.append(f"{fl / med / 1e9:10.1f}")
+            cells.append(f"{fl / med / 1e9:12.1f}")
+        cells.append("  us: " + " ".join(f"{statistics.median(res[(name, v)]) * 1e3:.1f}" for v in variants))
         print(f"{name:16s} {f'{M}x{N}x{K}':>22s} {batch:5d} " + " ".join(cells))
 
 
