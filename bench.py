@@ -144,20 +144,25 @@ def region_bytes(cfg, name: str) -> float:
     BL = B * L
     if name == "deinterleave":  # fp32 X read; bf16 plane 0 of 3 blocks (plane modes) or fp32 xs
         return B * D * (12.0 + (6.0 if np_ else 12.0))
-    if name == "eps_rng":
-        return 3 * BL * 4.0
-    if name == "latent_fwd":    # ms (mu, s) + eps in; z + its planes out
-        return 3 * BL * (8.0 + 4.0 + 4.0 + 2.0 * np_)
+    if name == "eps_rng":       # caller-given eps copied once (internal draws: no kernel)
+        return 3 * BL * 8.0
+    # the fused latent head (magic_amd/csrc/mvae_kernels.hip): eps regenerated from the Philox
+    # stream inside the kernels, z recomputed in the backward instead of stored and re-read
+    cos = cfg.metric == "cosine"
+    zl = 2.0 * np_ if (np_ and L >= 64) else 4.0   # lock z in the decoder GEMMs' operand format
+    if name == "latent_fwd":    # mu, s of 3 passes in; lock z (+ fp32 lock/key rows: cosine), row sums out
+        return 3 * BL * 8.0 + BL * (8.0 if cos else zl) + B * 16.0
     if name == "colsq":
         return 2 * BL * 4.0
-    if name == "metric_loss":   # z (3 blocks) + lock mu, s + areas/rowpart in; 4 row values out
-        return 3 * BL * 4.0 + 2 * BL * 4.0 + B * 4.0 * 6
+    if name == "metric_loss":   # row sums, BCE row partials, areas (+ cosine: lock/key rows); 3 row values out
+        nblk = (D + 127) // 128
+        return B * (16.0 + 4.0 * nblk + 4.0 + 12.0) + (2 * BL * 4.0 if cos else 0.0)
     if name == "coldot":
         return 2 * BL * 4.0 + B * 4.0
-    if name == "latent_bwd":    # z (3 blocks), lock mu/s + rot/key s, eps (3), dz_dec in; dhead (4 rows x 2L) out
+    if name == "latent_bwd":    # mu, s of 3 passes + dz_dec in; dhead (4 rows x 2L) out
         # (fp32 dhead rows only when a native-fp32 head GEMM reads them: f32 mode, or 2L < 256)
         d32 = 4.0 if (np_ == 0 or 2 * L < 256) else 0.0
-        return BL * (12.0 + 16.0 + 12.0 + 4.0) + 4 * BL * 2 * (d32 + 2.0 * np_)
+        return BL * (24.0 + 4.0) + 4 * BL * 2 * (d32 + 2.0 * np_)
     if cfg.conv:  # the conv tower's per-pixel kernels (magic_amd/csrc/conv_tower.hip)
         S1 = cfg.image_size // 2
         A1 = S1 * S1 * 64.0                # elements of one image after pool 1
@@ -627,7 +632,8 @@ def main():
                 loss_roofline[k] = {"bytes": by, "avg_ms": round(ms_k, 4),
                                     "gbs": round(by / (ms_k * 1e-3) / 1e9, 1),
                                     "frac": round(by / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-            lat = [k for k in ("latent_fwd", "colsq", "metric_loss", "coldot", "latent_bwd") if k in regions]
+            lat = [k for k in ("eps_rng", "latent_fwd", "colsq", "metric_loss", "coldot", "latent_bwd")
+                   if k in regions]
             ms_lat = sum(regions[k][0] / regions[k][1] for k in lat)
             by_lat = 80.0 * cfg.latent * cfg.batch
             loss_roofline["latent_head_total"] = {

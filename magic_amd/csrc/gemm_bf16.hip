@@ -899,7 +899,8 @@ bool wide_epi_vec_ok(const Params& g) {
   const GemmEpi& e = g.epi;
   if (e.c32 && (!al(g.C) || (g.ldc & 3) || (g.sC & 3))) return false;
   if (e.cp && (!al(e.cp) || (g.ldc & 7) || (g.sC & 7) || (e.pc & 7))) return false;
-  if (e.mode == EPI_DACT && (!al(e.aux) || (e.ld_aux & 3))) return false;
+  if (e.mode == EPI_DACT && !e.auxp && (!al(e.aux) || (e.ld_aux & 3))) return false;
+  if (e.mode == EPI_DACT && e.auxp && (!al(e.auxp) || (e.ld_aux & 7))) return false;
   if (e.mode == EPI_BCE || e.mode == EPI_BCEB) {
     if (e.x && (!al(e.x) || (e.ldx & 3))) return false;
     if (e.xp && (!al(e.xp) || (e.ldx & 7))) return false;

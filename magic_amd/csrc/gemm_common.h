@@ -25,9 +25,21 @@ struct Params {
 };
 constexpr int TN_TWIN = 1;  // Params::tn of the 128 x 128 twin kernel (gemm_bf16.hip)
 
+// tanh from the hardware exp / reciprocal (v_exp_f32, v_rcp_f32) and an odd polynomial where
+// 1 - 2/(e^2x + 1) cancels: relative error < 2e-6 everywhere (the accurate tanhf costs ~50 VALU
+// instructions per element, which the hidden-layer epilogues could not hide)
+__device__ __forceinline__ float tanh_fast(float x) {
+  const float ax = fabsf(x);
+  if (ax < 0.125f) {  // Taylor to x^7; the x^9 term is < 3e-10 |x| here
+    const float x2 = x * x;
+    return x * (1.f + x2 * (-0.333333333f + x2 * (0.133333333f + x2 * -0.0539682540f)));
+  }
+  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * ax) + 1.f);
+  return copysignf(t, x);
+}
 __device__ __forceinline__ float act_f(float v, int act) {
-  if (act == ACT_TANH) return tanhf(v);
-  return v < 0.f ? expf(v) - 1.f : v;  // TF elu: exp(x) - 1 for x < 0
+  if (act == ACT_TANH) return tanh_fast(v);
+  return v < 0.f ? __expf(v) - 1.f : v;  // TF elu: exp(x) - 1 for x < 0
 }
 __device__ __forceinline__ float dact_f(float g, float y, int act) {
   if (act == ACT_TANH) return g * (1.f - y * y);  // TF TanhGrad
@@ -144,6 +156,8 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
           int col = cbase + ni * 32;
           col = col < p.N ? col : p.N - 1;
           if constexpr (EPI == EPI_BCEB) sv[r][ni] = bf16_bits_to_f32(e.xp[(size_t)sr * lds_ + col]);
+          else if constexpr (EPI == EPI_DACT)
+            sv[r][ni] = e.auxp ? bf16_bits_to_f32(e.auxp[(size_t)sr * lds_ + col]) : src[(size_t)sr * lds_ + col];
           else sv[r][ni] = src[(size_t)sr * lds_ + col];
         }
       }
@@ -292,11 +306,27 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
         float sv[8];
         if constexpr (EPI == EPI_DACT) {
           const int ar = row >= e.remap_split ? row - e.remap_shift : row;
-          const float* src = e.aux + (size_t)ar * e.ld_aux + col0;
-          if (full) ld8f(src, sv);
-          else
+          if (e.auxp) {  // the activation's bf16 plane (bf16 mode: no fp32 copy is written)
+            const unsigned short* src = e.auxp + (size_t)ar * e.ld_aux + col0;
+            if (full) {
+              const uint4 w = *reinterpret_cast<const uint4*>(src);
+              const unsigned ww[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
-            for (int j = 0; j < 8; ++j) sv[j] = j < nv ? src[j] : 0.f;
+              for (int j = 0; j < 4; ++j) {
+                sv[2 * j] = __uint_as_float(ww[j] << 16);
+                sv[2 * j + 1] = __uint_as_float(ww[j] & 0xffff0000u);
+              }
+            } else {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) sv[j] = j < nv ? bf16_bits_to_f32(src[j]) : 0.f;
+            }
+          } else {
+            const float* src = e.aux + (size_t)ar * e.ld_aux + col0;
+            if (full) ld8f(src, sv);
+            else
+#pragma unroll
+              for (int j = 0; j < 8; ++j) sv[j] = j < nv ? src[j] : 0.f;
+          }
         }
         if constexpr (EPI == EPI_BCE) {
           const float* src = e.x + (size_t)row * e.ldx + col0;

@@ -216,7 +216,8 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, in
     if constexpr (EPI == EPI_SIGMOID) v = sigmoid_f(v);
     if constexpr (EPI == EPI_DACT) {
       const int ar = row >= e.remap_split ? row - e.remap_shift : row;
-      v = dact_f(v, e.aux[(size_t)ar * e.ld_aux + col], e.act);
+      const size_t ai = (size_t)ar * e.ld_aux + col;
+      v = dact_f(v, e.auxp ? bf16_bits_to_f32(e.auxp[ai]) : e.aux[ai], e.act);
     }
     if (e.c32) c[(size_t)row * ldc + col] = v;
     if (e.cp) store_planes(e.cp + bi * sC, e.pc, e.ncp, (size_t)row * ldc + col, v);
@@ -261,9 +262,14 @@ __global__ void splitk_reduce4_kernel(const float* __restrict__ ws, int split, i
     }
     if constexpr (EPI == EPI_DACT) {
       const int ar = row >= e.remap_split ? row - e.remap_shift : row;
-      const float* x = e.aux + (size_t)ar * e.ld_aux + col;
+      const size_t ai = (size_t)ar * e.ld_aux + col;
+      if (e.auxp) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = dact_f(v[j], x[j], e.act);
+        for (int j = 0; j < 4; ++j) v[j] = dact_f(v[j], bf16_bits_to_f32(e.auxp[ai + j]), e.act);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = dact_f(v[j], e.aux[ai + j], e.act);
+      }
     }
     const size_t o = (size_t)row * ldc + col;
     if (e.c32) *reinterpret_cast<float4*>(c + o) = make_float4(v[0], v[1], v[2], v[3]);

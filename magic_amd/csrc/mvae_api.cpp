@@ -68,6 +68,10 @@ struct mvae_ctx {
   float *ms = nullptr, *z = nullptr, *a1 = nullptr, *a2 = nullptr, *du = nullptr;
   float *rowpart = nullptr, *rowvals = nullptr, *dist = nullptr, *draw = nullptr, *losses = nullptr;
   float *colsq = nullptr, *coldot = nullptr, *cspart = nullptr, *eps = nullptr;
+  float* rowfwd = nullptr;   // [B][4] latent forward row sums (KL, deformation, sq-diff distance)
+  LatentEps le;              // eps of the last forward (buffer, or the Philox call regenerated)
+  bool eps_lazy = false;     // le is a Philox call whose values the eps buffer does not hold yet
+  int zmask = 6;             // fp32 z rows the latent forward writes (bit 1 lock, bit 2 key)
   float *dzd2 = nullptr, *dzd1 = nullptr, *dzdec = nullptr, *dhead = nullptr;
   std::vector<float*> dzl;  // dZ of every encoder layer [4B][lddz] (all live until its wgrad)
   int enc_part1 = 0;        // bwd_enc[0, enc_part1): dgrad chain + layer-0 wgrad
@@ -471,6 +475,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   ALLOC(c->coldot, L);
   ALLOC(c->cspart, (size_t)c->nchunk * 2 * L);
   ALLOC(c->eps, 3 * B * L);
+  ALLOC(c->rowfwd, 4 * B);
   ALLOC(c->dzd2, B * c->ld_d2);
   ALLOC(c->dzd1, B * c->ld_d1);
   ALLOC(c->dzdec, B * L);
@@ -533,6 +538,8 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   // kernel A/B switch (diagnostics): MVAE_TWIN=0 plans the bf16 DMA GEMMs on the ring kernels
   // only (round-2 plan), 2 forces the 128x128 twin kernel wherever a ring kernel would run
   int twin_mode = 1;
+  bool dact_planes = true;  // MVAE_DACT_F32AUX=1: bf16-mode DACT reads the fp32 activations (A/B)
+  if (const char* fa = std::getenv("MVAE_DACT_F32AUX"); fa && *fa == '1') dact_planes = false;
   if (const char* tw = std::getenv("MVAE_TWIN"); tw && (*tw == '0' || *tw == '2')) twin_mode = *tw - '0';
   const int gp = cfg->precision == MVAE_PREC_BF16 ? GEMM_BF16
                  : (cfg->precision == MVAE_PREC_F32X ? GEMM_F32X : GEMM_F32);
@@ -592,6 +599,11 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     if (gp == GEMM_F32X && !gemm_bf16_wide(d)) d.prec = GEMM_F32;
     if (d.prec != GEMM_F32 && !d.valu && gemm_bf16_wide(d) && twin_mode != 1)
       d.variant = twin_mode == 0 ? 15 : 13;
+    // bf16 mode: a plane-kernel DACT epilogue reads the activation's bf16 plane (act' from the
+    // bf16-rounded output, the operand precision of this mode), so the forward epilogues write
+    // the activations as planes only (no fp32 copy)
+    if (c->np == 1 && d.epi.mode == EPI_DACT && d.prec != GEMM_F32 && !d.valu && dact_planes)
+      d.epi.auxp = planes_of(c, d.epi.aux).p;
   };
   for (auto* v : {&c->fwd_enc, &c->bwd_dec, &c->bwd_enc})
     for (auto& d : *v) wire(d);
@@ -632,10 +644,16 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
       bool fp32_reader = false;
       for (const GemmDesc* g : all) {
         if (g->prec == GEMM_F32 && (in(g->A) || in(g->B))) fp32_reader = true;
-        if (g->epi.mode == EPI_DACT && in(g->epi.aux)) fp32_reader = true;
+        if (g->epi.mode == EPI_DACT && in(g->epi.aux) && !g->epi.auxp) fp32_reader = true;
       }
       d->epi.c32 = fp32_reader ? 1 : 0;
     }
+  }
+  {  // fp32 z rows: lock for fp32 decoder GEMMs (layer-1 forward, its weight gradient) and the
+     // cosine column statistics; key for the cosine statistics only
+    const bool cos = cfg->metric == MVAE_METRIC_COSINE;
+    const bool lock32 = !c->np || cos || c->f_d1.prec == GEMM_F32 || c->bwd_dec[4].prec == GEMM_F32;
+    c->zmask = (lock32 ? 2 : 0) | (cos ? 4 : 0);
   }
   if (c->np) {  // fp32 dhead only for a native-fp32 head GEMM (else its planes alone)
     c->dhead32 = 0;
@@ -789,7 +807,17 @@ int mvae_buffer(mvae_ctx* ctx, int which, float** ptr, size_t* count) {
     case MVAE_BUF_DIST: *ptr = ctx->dist; *count = ctx->B; break;
     case MVAE_BUF_GRADS_DEC: *ptr = ctx->grads + ctx->n_enc; *count = ctx->n_all - ctx->n_enc; break;
     case MVAE_BUF_DEAD: *ptr = ctx->dead; *count = (size_t)ctx->d1 * ctx->D + ctx->D; break;
-    case MVAE_BUF_EPS: *ptr = ctx->eps; *count = (size_t)3 * ctx->B * ctx->L; break;
+    case MVAE_BUF_EPS:
+      if (ctx->eps_lazy) {  // the last forward's internal draw, written out on request
+        hipError_t e = hipDeviceSynchronize();
+        if (e == hipSuccess)
+          e = launch_normal(ctx->eps, 3, ctx->B, ctx->L, ctx->le.Bg, ctx->le.off, ctx->le.seed,
+                            ctx->le.counter, nullptr);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) return fail(ctx, (int)e, std::string("eps: ") + hipGetErrorString(e));
+        ctx->eps_lazy = false;
+      }
+      *ptr = ctx->eps; *count = (size_t)3 * ctx->B * ctx->L; break;
     case MVAE_BUF_DYN:
       if (!ctx->dyn) return fail(ctx, MVAE_EINVAL, "no dyn flag in this precision mode");
       *ptr = reinterpret_cast<float*>(ctx->dyn); *count = 1; break;
@@ -875,16 +903,22 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
   }
   const size_t ne = (size_t)3 * c->B * c->L;
   if (draw != ENC_MEAN) {
-    TIMED("eps_rng");
+    // eps of this forward: the caller's draws (copied: the backward needs them after the
+    // caller's buffer may be gone), or the next call of the training / inference Philox
+    // stream, regenerated inside the latent kernels (no eps buffer traffic)
+    LatentEps le;
+    le.seed = c->cfg.seed;
+    le.Bg = c->cfg.global_batch;
+    le.off = c->row_off;
     if (eps) {
+      TIMED("eps_rng");
       MV_CHECK(hipMemcpyAsync(c->eps, eps, ne * sizeof(float), hipMemcpyDeviceToDevice, st));
-    } else if (draw == ENC_TRAIN) {
-      MV_CHECK(launch_normal(c->eps, 3, c->B, c->L, c->cfg.global_batch, c->row_off, c->cfg.seed,
-                             c->rng_counter++, st));
+      le.buf = c->eps;
     } else {
-      MV_CHECK(launch_normal(c->eps, 3, c->B, c->L, c->cfg.global_batch, c->row_off, c->cfg.seed,
-                             EVAL_STREAM | c->rng_eval++, st));
+      le.counter = draw == ENC_TRAIN ? c->rng_counter++ : (EVAL_STREAM | c->rng_eval++);
     }
+    c->eps_lazy = le.buf == nullptr;
+    c->le = le;
   }
   if (c->conv) {  // the tower: xs pixels -> xf features (the FC layer-0 operand)
     const ConvTower& T = c->tower;
@@ -911,7 +945,8 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
   if (draw == ENC_MEAN) return MVAE_OK;
   {
     TIMED("latent_fwd");
-    MV_CHECK(launch_latent_fwd(c->ms, c->eps, c->z, planes_of(c, c->z), c->B, c->L, c->ldz, st));
+    MV_CHECK(launch_latent_fwd(c->ms, c->le, c->z, planes_of(c, c->z), c->zmask, c->B, c->L, c->ldz,
+                               c->rowfwd, st));
   }
   if (c->cfg.metric == MVAE_METRIC_COSINE) {
     TIMED("colsq");
@@ -940,7 +975,7 @@ extern "C" int mvae_metric(mvae_ctx* ctx, const float* areas, void* stream) {
   auto c = ctx;
   {
     TIMED("metric_loss");
-    MV_CHECK(launch_metric(c->z, c->ldz, c->ms, c->rowpart, c->nblk, areas, c->colsq, c->B, c->L,
+    MV_CHECK(launch_metric(c->z, c->ldz, c->rowfwd, c->rowpart, c->nblk, areas, c->colsq, c->B, c->L,
                            c->cfg.metric, c->cfg.reciprocal, c->cfg.deform_weight, c->inv_bg,
                            c->rowvals, c->dist, c->draw, st));
     MV_CHECK(launch_loss_reduce(c->rowvals, c->B, c->inv_bg, c->losses, st));
@@ -992,7 +1027,7 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
   } else if (part == 1) {
     {
       TIMED("latent_bwd");
-      MV_CHECK(launch_latent_bwd(c->z, c->ldz, c->ms, c->eps, c->dzdec, c->draw, c->colsq, c->coldot,
+      MV_CHECK(launch_latent_bwd(c->ms, c->le, c->dzdec, c->draw, c->colsq, c->coldot,
                                  c->B, c->L, c->cfg.metric, c->cfg.deform_weight, c->inv_bg,
                                  c->dhead32 ? c->dhead : nullptr,
                                  c->ld_dh, planes_of(c, c->dhead), st));
@@ -1140,7 +1175,7 @@ extern "C" int mvae_predict_finish(mvae_ctx* ctx, float* dist_out, void* stream)
   if (ctx->phase != 6) return fail(ctx, MVAE_ESTATE, "mvae_predict_finish before mvae_predict_encode");
   hipStream_t st = (hipStream_t)stream;
   auto c = ctx;
-  MV_CHECK(launch_metric(c->z, c->ldz, c->ms, c->rowpart, c->nblk, nullptr, c->colsq, c->B, c->L,
+  MV_CHECK(launch_metric(c->z, c->ldz, c->rowfwd, c->rowpart, c->nblk, nullptr, c->colsq, c->B, c->L,
                          c->cfg.metric, c->cfg.reciprocal, c->cfg.deform_weight, c->inv_bg,
                          c->rowvals, dist_out, c->draw, st));
   ctx->phase = 0;
@@ -1340,9 +1375,13 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   if (M <= 0 || N <= 0 || K <= 0 || iters <= 0 || !avg_ms || batch <= 0) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   // operand rows padded to 8 elements (16 B), as the step's buffers are
-  const int lda = ((at ? M : K) + 7) & ~7, ldb = ((bt ? K : N) + 7) & ~7;
+  // MVAE_BENCH_LDPAD (diagnostics): row strides rounded to this many elements (default 8)
+  int pad = 8;
+  if (const char* lp = std::getenv("MVAE_BENCH_LDPAD"); lp && std::atoi(lp) >= 8) pad = std::atoi(lp) & ~7;
+  auto rnd = [&](int v) { return (v + pad - 1) / pad * pad; };
+  const int lda = rnd(at ? M : K), ldb = rnd(bt ? K : N);
   const size_t sa = (size_t)(at ? K : M) * lda, sb = (size_t)(bt ? N : K) * ldb;
-  const int ldc = (N + 7) & ~7;  // output rows padded to 16 B as well (the 16-B epilogue stores)
+  const int ldc = rnd(N);  // output rows padded to 16 B as well (the 16-B epilogue stores)
   const size_t na = sa * batch, nb = sb * batch, nc = (size_t)M * ldc * batch;
   float *A = nullptr, *Bm = nullptr, *Cm = nullptr, *ws = nullptr;
   GemmDesc d = gd(M, N, K, nullptr, lda, at != 0, nullptr, ldb, bt != 0, nullptr, ldc);

@@ -29,6 +29,9 @@ struct GemmEpi {
   int act = ACT_TANH;
   const float* aux = nullptr;   // DACT: activation output the gradient flows through
   int ld_aux = 0;
+  // DACT: bf16 plane 0 of aux (same ld), read instead of aux when set (bf16 mode: the
+  // activations are then stored as bf16 planes only)
+  const unsigned short* auxp = nullptr;
   int remap_split = 1 << 30;    // aux row = row >= remap_split ? row - remap_shift : row
   int remap_shift = 0;
   const float* x = nullptr;     // BCE: target pixels (lock image), fp32
@@ -105,21 +108,31 @@ hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int*
 // (Bg rows per slot over all ranks, this rank's rows starting at off)
 hipError_t launch_normal(float* out, int slots, int B, int L, int Bg, int off, uint64_t seed,
                          uint64_t counter, hipStream_t st);
-hipError_t launch_latent_fwd(const float* ms, const float* eps, float* z, const Planes& zp, int B,
-                             int L, int ldz, hipStream_t st);
+// eps of the latent head: the [3][B][L] buffer `buf` (caller-given draws), or, when buf is
+// NULL, the Philox stream (seed, counter) regenerated inside the kernels at this rank's rows
+// (global batch Bg, first row off): the same values launch_normal would write.
+struct LatentEps {
+  const float* buf = nullptr;
+  uint64_t seed = 0, counter = 0;
+  int Bg = 0, off = 0;
+};
+// Fused latent forward (one wave per row): z = mu + sqrt(exp s) eps for the three passes,
+// z written where read (zmask bit 1: fp32 lock rows, bit 2: fp32 key rows; zp: lock planes),
+// rowfwd[b] = {sum KL term, sum (z_lock - z_rot)^2, sum (z_lock - z_key)^2, 0}.
+hipError_t launch_latent_fwd(const float* ms, const LatentEps& eps, float* z, const Planes& zp,
+                             int zmask, int B, int L, int ldz, float* rowfwd, hipStream_t st);
 // out[j] for j in [0, ncols): mode 0 = colsq (z_lock^2 | z_key^2), mode 1 = coldot.
 hipError_t launch_colstats(int mode, const float* z, int B, int L, int ldz, const float* colsq,
                            const float* draw, float* part, int nchunk, float* out, hipStream_t st);
 int colstats_nchunk(int B);
-hipError_t launch_metric(const float* z, int ldz, const float* ms, const float* rowpart, int nblk,
+hipError_t launch_metric(const float* z, int ldz, const float* rowfwd, const float* rowpart, int nblk,
                          const float* areas, const float* colsq, int B, int L, int metric, int recip,
                          float w, float inv_bg, float* rowvals, float* dist, float* draw,
                          hipStream_t st);
 hipError_t launch_loss_reduce(const float* rowvals, int B, float inv_bg, float* losses, hipStream_t st);
-hipError_t launch_latent_bwd(const float* z, int ldz, const float* ms, const float* eps,
-                             const float* dzdec, const float* draw, const float* colsq,
-                             const float* coldot, int B, int L, int metric, float w, float inv_bg,
-                             float* dhead, int ldh, const Planes& hp, hipStream_t st);
+hipError_t launch_latent_bwd(const float* ms, const LatentEps& eps, const float* dzdec, const float* draw,
+                             const float* colsq, const float* coldot, int B, int L, int metric, float w,
+                             float inv_bg, float* dhead, int ldh, const Planes& hp, hipStream_t st);
 struct AdamArgs {
   float* theta; const float* g1; const float* g2; float* m1; float* v1; float* m2; float* v2;
   size_t n_all, n_enc; float lr1, lr2, b1, b2, eps;

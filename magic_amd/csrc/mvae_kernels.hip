@@ -149,6 +149,26 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
   }
 }
 
+// The 4 normals of Philox block q of call `counter`: global elements 4q .. 4q+3 of the stream
+// (Box-Muller on the block's two 32-bit pairs). The sampler kernel and the fused latent kernels
+// (which regenerate eps in registers instead of reading it) share this code, so a regenerated
+// value is bit-identical to the sampled one.
+__device__ __forceinline__ void normal4(uint64_t q, uint64_t seed, uint64_t counter, float (&r)[4]) {
+  uint32_t c[4] = {(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)counter, (uint32_t)(counter >> 32)};
+  philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+  const float inv = 2.3283064365386963e-10f;  // 2^-32
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const float u1 = __fmul_rn(__fadd_rn((float)c[2 * j], 0.5f), inv);  // (0,1)
+    const float u2 = __fmul_rn(__fadd_rn((float)c[2 * j + 1], 0.5f), inv);
+    const float rad = sqrtf(__fmul_rn(-2.f, logf(u1)));
+    float sn, co;
+    sincosf(__fmul_rn(6.283185307179586f, u2), &sn, &co);
+    r[2 * j] = __fmul_rn(rad, co);
+    r[2 * j + 1] = __fmul_rn(rad, sn);
+  }
+}
+
 // One Philox block per thread -> 4 normals at consecutive GLOBAL element indices. With a
 // row-sharded batch the rank's elements of slot s (blockIdx.y) are the contiguous global range
 // [(s*Bg + off)*L, +B*L): a data-parallel rank draws exactly its slice of the eps the single
@@ -159,20 +179,8 @@ __global__ void normal_kernel(float* __restrict__ out, int B, int L, int Bg, int
   const size_t g0 = ((size_t)blockIdx.y * Bg + off) * L;  // first global element of this slot
   const size_t q = g0 / 4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;  // Philox block
   if (4 * q >= g0 + n) return;
-  uint32_t c[4] = {(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)counter, (uint32_t)(counter >> 32)};
-  philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
-  const float inv = 2.3283064365386963e-10f;  // 2^-32
   float r[4];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const float u1 = ((float)c[2 * j] + 0.5f) * inv;  // (0,1)
-    const float u2 = ((float)c[2 * j + 1] + 0.5f) * inv;
-    const float rad = sqrtf(-2.f * logf(u1));
-    float s, co;
-    sincosf(6.283185307179586f * u2, &s, &co);
-    r[2 * j] = rad * co;
-    r[2 * j + 1] = rad * s;
-  }
+  normal4(q, seed, counter, r);
   float* o = out + (size_t)blockIdx.y * n;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -181,45 +189,138 @@ __global__ void normal_kernel(float* __restrict__ out, int B, int L, int Bg, int
   }
 }
 
-// ---------------------------------------------------------------- reparameterisation
-// z = mu + sqrt(exp(s)) * eps   (11a/vae.py:371-377); ms rows = [mu | s] (2L wide). The bf16
-// planes of z are written for the lock block only: the decoder's GEMMs read no other rows.
-__global__ void latent_fwd_kernel(const float* __restrict__ ms, const float* __restrict__ eps,
-                                  float* __restrict__ z, unsigned short* __restrict__ zp,
-                                  long long ps, int np, int B, int L, int ldz) {
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (size_t)3 * B * L) return;
-  const int r = (int)(idx / L), i = (int)(idx - (size_t)r * L);
-  const int blk = r / B, b = r - blk * B;
-  const float mu = ms[(size_t)r * 2 * L + i];
-  const float s = ms[(size_t)r * 2 * L + L + i];
-  const float e = eps[((size_t)eps_slot(blk) * B + b) * L + i];
-  const float v = mu + sqrtf(expf(s)) * e;
-  z[(size_t)r * ldz + i] = v;
-  if (zp && blk == 1) planes_put(zp, ps, np, (size_t)r * ldz + i, v);
+// ---------------------------------------------------------------- fused latent head
+// eps of the reparameterisation (11a/vae.py:373): the [3][B][L] buffer (given by the caller),
+// or the training / inference Philox stream regenerated in registers (internal draws: no eps
+// buffer is written or read; mvae_buffer(MVAE_BUF_EPS) materialises it on demand).
+struct EpsSrc {
+  const float* buf;   // nullptr: regenerate
+  uint64_t seed, counter;
+  int Bg, off;        // global batch and this rank's first row (the sharded stream)
+};
+
+// eps of (internal block blk, row b, columns i .. i+3); V4: L % 4 == 0 and i % 4 == 0, so the
+// four elements are exactly one Philox block
+template <bool V4>
+__device__ __forceinline__ void eps_get(const EpsSrc& es, int blk, int b, int i, int B, int L,
+                                        float (&e)[4]) {
+  const int sl = eps_slot(blk);
+  if (es.buf) {
+    const float* p = es.buf + ((size_t)sl * B + b) * L + i;
+    if constexpr (V4) {
+      const float4 v = *reinterpret_cast<const float4*>(p);
+      e[0] = v.x; e[1] = v.y; e[2] = v.z; e[3] = v.w;
+    } else {
+      e[0] = p[0];
+    }
+    return;
+  }
+  const size_t g = ((size_t)sl * es.Bg + es.off + b) * L + i;  // global element
+  if constexpr (V4) {
+    normal4(g >> 2, es.seed, es.counter, e);
+  } else {
+    float r[4];
+    normal4(g >> 2, es.seed, es.counter, r);
+    e[0] = r[g & 3];
+  }
 }
 
-// the same, 4 consecutive elements per thread (L % 4 == 0: 16-B rows of ms, eps and z)
-__global__ void latent_fwd4_kernel(const float* __restrict__ ms, const float* __restrict__ eps,
-                                   float* __restrict__ z, unsigned short* __restrict__ zp,
-                                   long long ps, int np, int B, int L, int ldz) {
-  const int L4 = L / 4;
-  const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (size_t)3 * B * L4) return;
-  const int r = (int)(idx / L4), i = 4 * (int)(idx - (size_t)r * L4);
-  const int blk = r / B, b = r - blk * B;
-  const float4 mu = *reinterpret_cast<const float4*>(ms + (size_t)r * 2 * L + i);
-  const float4 s = *reinterpret_cast<const float4*>(ms + (size_t)r * 2 * L + L + i);
-  const float4 e = *reinterpret_cast<const float4*>(eps + ((size_t)eps_slot(blk) * B + b) * L + i);
-  const float4 v = make_float4(mu.x + sqrtf(expf(s.x)) * e.x, mu.y + sqrtf(expf(s.y)) * e.y,
-                               mu.z + sqrtf(expf(s.z)) * e.z, mu.w + sqrtf(expf(s.w)) * e.w);
-  const size_t o = (size_t)r * ldz + i;
-  *reinterpret_cast<float4*>(z + o) = v;
-  if (zp && blk == 1) {
-    planes_put(zp, ps, np, o, v.x);
-    planes_put(zp, ps, np, o + 1, v.y);
-    planes_put(zp, ps, np, o + 2, v.z);
-    planes_put(zp, ps, np, o + 3, v.w);
+// z = mu + sqrt(exp(s)) * eps (11a/vae.py:371-377), one explicit rounding sequence shared by
+// the forward and the backward (which recomputes z instead of reading it)
+__device__ __forceinline__ float reparam(float mu, float s, float e) {
+  return __fadd_rn(mu, __fmul_rn(sqrtf(expf(s)), e));
+}
+
+__device__ __forceinline__ void ld4(const float* p, float (&v)[4]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+}
+// 4 values -> n bf16 planes at p[t*ps + o .. +3] (8-B stores; o % 4 == 0)
+__device__ __forceinline__ void planes_put4(unsigned short* p, long long ps, int n, size_t o,
+                                            const float (&v)[4]) {
+  float r[4] = {v[0], v[1], v[2], v[3]};
+  for (int t = 0; t < n; ++t) {
+    unsigned short q[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      q[j] = __builtin_bit_cast(unsigned short, __float2bfloat16(r[j]));
+      r[j] -= __uint_as_float((unsigned)q[j] << 16);
+    }
+    *reinterpret_cast<uint2*>(p + t * ps + o) = pack4(q[0], q[1], q[2], q[3]);
+  }
+}
+
+// Forward of the latent head, one wave per batch row b (V4: 4 columns per lane): mu / s of the
+// three passes (ms rows [mu | s], 2L wide) and eps -> z, written only where something reads it
+// (zmask bit 1: fp32 lock row, for fp32 decoder GEMMs and the cosine statistics; bit 2: fp32 key
+// row, cosine only; the lock row's bf16 planes for the plane-mode decoder GEMMs), and the row
+// sums rowfwd[b] = {sum(1 + s - mu^2 - exp s) (KL, lock pass, :281-284), sum (z_lock - z_rot)^2
+// (deformation, :293-294), sum (z_lock - z_key)^2 (squared-difference distance, :309)}.
+// WPR waves per row: 1 (four rows per 256-thread workgroup) or 4 (one long row per workgroup,
+// the four waves' sums combined through LDS in a fixed order), so a 2000-wide row keeps enough
+// loads in flight.
+template <bool V4, int WPR>
+__global__ void latent_fwd_kernel(const float* __restrict__ ms, EpsSrc es, float* __restrict__ z,
+                                  unsigned short* __restrict__ zp, long long ps, int np, int zmask,
+                                  int B, int L, int ldz, float* __restrict__ rowfwd) {
+  const int lane = threadIdx.x & 63;
+  const int wr = (threadIdx.x >> 6) % WPR;  // wave within the row
+  const int b = blockIdx.x * (4 / WPR) + (threadIdx.x >> 6) / WPR;
+  __shared__ float red[4][3];
+  if (WPR == 1 && b >= B) return;
+  constexpr int W = V4 ? 4 : 1;
+  float kl = 0.f, fd = 0.f, sq = 0.f;
+  for (int i = W * (lane + 64 * wr); i < L; i += 64 * W * WPR) {
+    float zz[3][4], mul[4], sl[4];
+#pragma unroll
+    for (int blk = 0; blk < 3; ++blk) {
+      const float* row = ms + (size_t)(blk * B + b) * 2 * L;
+      float mu[4], sg[4], e[4];
+      if constexpr (V4) { ld4(row + i, mu); ld4(row + L + i, sg); }
+      else { mu[0] = row[i]; sg[0] = row[L + i]; }
+      eps_get<V4>(es, blk, b, i, B, L, e);
+#pragma unroll
+      for (int j = 0; j < W; ++j) zz[blk][j] = reparam(mu[j], sg[j], e[j]);
+      if (blk == 1) {
+#pragma unroll
+        for (int j = 0; j < W; ++j) { mul[j] = mu[j]; sl[j] = sg[j]; }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < W; ++j) {
+      kl += 1.f + sl[j] - mul[j] * mul[j] - expf(sl[j]);
+      const float d = zz[1][j] - zz[0][j], q = zz[1][j] - zz[2][j];
+      fd += d * d;
+      sq += q * q;
+    }
+    const size_t ol = (size_t)(B + b) * ldz + i, ok = (size_t)(2 * B + b) * ldz + i;
+    if constexpr (V4) {
+      if (zmask & 2) *reinterpret_cast<float4*>(z + ol) = make_float4(zz[1][0], zz[1][1], zz[1][2], zz[1][3]);
+      if (zmask & 4) *reinterpret_cast<float4*>(z + ok) = make_float4(zz[2][0], zz[2][1], zz[2][2], zz[2][3]);
+      if (zp) planes_put4(zp, ps, np, ol, zz[1]);
+    } else {
+      if (zmask & 2) z[ol] = zz[1][0];
+      if (zmask & 4) z[ok] = zz[2][0];
+      if (zp) planes_put(zp, ps, np, ol, zz[1][0]);
+    }
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) {
+    kl += __shfl_xor(kl, off, 64);
+    fd += __shfl_xor(fd, off, 64);
+    sq += __shfl_xor(sq, off, 64);
+  }
+  if constexpr (WPR == 1) {
+    if (lane == 0) *reinterpret_cast<float4*>(rowfwd + 4 * (size_t)b) = make_float4(kl, fd, sq, 0.f);
+  } else {
+    if (lane == 0) { red[wr][0] = kl; red[wr][1] = fd; red[wr][2] = sq; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      float t[3];
+#pragma unroll
+      for (int q = 0; q < 3; ++q) t[q] = ((red[0][q] + red[1][q]) + red[2][q]) + red[3][q];
+      *reinterpret_cast<float4*>(rowfwd + 4 * (size_t)b) = make_float4(t[0], t[1], t[2], 0.f);
+    }
   }
 }
 
@@ -272,11 +373,12 @@ __global__ void colstats_final_kernel(const float* __restrict__ part, int nchunk
 // ---------------------------------------------------------------- metric / losses per row
 // One wave per batch row b. rowvals[b] = {R_b, K_b, F_b, T_b}; dist[b]; draw[b] = dT/draw_b.
 //   R_b: BCE row partials from the decoder-output GEMM epilogue (11a/vae.py:266-269)
-//   K_b = -0.5 sum(1 + s - mu^2 - exp(s))            (lock pass, :281-284)
-//   F_b = w sum (z_lock - z_rot)^2                    (:293-294)
-//   dist_b: cosine (axis-0 l2_normalize, :444-458) or sum (z_lock - z_key)^2; 1/raw if recip
+//   K_b = -0.5 sum(1 + s - mu^2 - exp(s)), F_b = w sum (z_lock - z_rot)^2: the fused latent
+//         forward's row sums (rowfwd, :281-284, :293-294)
+//   dist_b: sum (z_lock - z_key)^2 (rowfwd) or cosine (axis-0 l2_normalize, :444-458, from the
+//         fp32 lock / key rows and the column sums of squares); 1/raw if recip
 //   T_b = (dist_b - area_b)^2                         (:313)
-__global__ void metric_kernel(const float* __restrict__ z, int ldz, const float* __restrict__ ms,
+__global__ void metric_kernel(const float* __restrict__ z, int ldz, const float* __restrict__ rowfwd,
                               const float* __restrict__ rowpart, int nblk,
                               const float* __restrict__ areas, const float* __restrict__ colsq,
                               int B, int L, int metric, int recip, float w, float inv_bg,
@@ -285,54 +387,43 @@ __global__ void metric_kernel(const float* __restrict__ z, int ldz, const float*
   const int lane = threadIdx.x & 63;
   const int b = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
   if (b >= B) return;
-  const float* zr = z + (size_t)b * ldz;
   const float* zl = z + (size_t)(B + b) * ldz;
   const float* zk = z + (size_t)(2 * B + b) * ldz;
-  const float* msl = ms + (size_t)(B + b) * 2 * L;
-  float kl = 0.f, fd = 0.f, raw = 0.f, rp = 0.f;
-  auto term = [&](float mu, float s, float l, float r, float k, int i) {
-    kl += 1.f + s - mu * mu - expf(s);
-    const float d = l - r;
-    fd += d * d;
-    if (metric == 0) {
+  float raw = 0.f, rp = 0.f;
+  if (metric == 0) {
+    auto term = [&](float l, float k, int i) {
       const float rl = rsqrtf(fmaxf(colsq[i], L2_EPS));
       const float rk = rsqrtf(fmaxf(colsq[L + i], L2_EPS));
       raw += (l * rl) * (k * rk);
+    };
+    if ((L & 3) == 0 && L >= 256 && (ldz & 3) == 0) {  // 16-B loads, 4 elements per lane
+      for (int i = 4 * lane; i < L; i += 256) {
+        const float4 l = *reinterpret_cast<const float4*>(zl + i);
+        const float4 k = *reinterpret_cast<const float4*>(zk + i);
+        term(l.x, k.x, i);
+        term(l.y, k.y, i + 1);
+        term(l.z, k.z, i + 2);
+        term(l.w, k.w, i + 3);
+      }
     } else {
-      const float e = l - k;
-      raw += e * e;
+      for (int i = lane; i < L; i += 64) term(zl[i], zk[i], i);
     }
-  };
-  if ((L & 3) == 0 && L >= 256 && (ldz & 3) == 0) {  // 16-B loads, 4 elements per lane (all lanes busy)
-    for (int i = 4 * lane; i < L; i += 256) {
-      const float4 mu = *reinterpret_cast<const float4*>(msl + i);
-      const float4 s = *reinterpret_cast<const float4*>(msl + L + i);
-      const float4 l = *reinterpret_cast<const float4*>(zl + i);
-      const float4 r = *reinterpret_cast<const float4*>(zr + i);
-      const float4 k = *reinterpret_cast<const float4*>(zk + i);
-      term(mu.x, s.x, l.x, r.x, k.x, i);
-      term(mu.y, s.y, l.y, r.y, k.y, i + 1);
-      term(mu.z, s.z, l.z, r.z, k.z, i + 2);
-      term(mu.w, s.w, l.w, r.w, k.w, i + 3);
-    }
-  } else {
-    for (int i = lane; i < L; i += 64) term(msl[i], msl[L + i], zl[i], zr[i], zk[i], i);
   }
   for (int j = lane; j < nblk; j += 64) rp += rowpart[(size_t)b * nblk + j];
 #pragma unroll
   for (int off = 32; off >= 1; off >>= 1) {
-    kl += __shfl_xor(kl, off, 64);
-    fd += __shfl_xor(fd, off, 64);
     raw += __shfl_xor(raw, off, 64);
     rp += __shfl_xor(rp, off, 64);
   }
   if (lane == 0) {
+    const float4 f = *reinterpret_cast<const float4*>(rowfwd + 4 * (size_t)b);
+    if (metric == 1) raw = f.z;
     const float dv = recip ? 1.f / raw : raw;
     const float a = areas ? areas[b] : 0.f;
     const float g = 2.f * (dv - a) * inv_bg;
     rowvals[4 * (size_t)b + 0] = rp;
-    rowvals[4 * (size_t)b + 1] = -0.5f * kl;
-    rowvals[4 * (size_t)b + 2] = w * fd;
+    rowvals[4 * (size_t)b + 1] = -0.5f * f.x;
+    rowvals[4 * (size_t)b + 2] = w * f.y;
     rowvals[4 * (size_t)b + 3] = (dv - a) * (dv - a);
     dist[b] = dv;
     draw[b] = recip ? -g * dv * dv : g;  // tf.reciprocal grad: -dy * y^2
@@ -376,60 +467,75 @@ __global__ void loss_reduce_kernel(const float* __restrict__ rowvals, int B, flo
 //       cosine: dz = r (draw n_other - n c), c = coldot (summed over the global batch),
 //               the n*c term only where sum z^2 >= 1e-12 (tf.maximum routes the gradient)
 //   reparameterisation: dmu = dz, ds = 0.5 dz eps sigma
-__global__ void latent_bwd_kernel(const float* __restrict__ z, int ldz, const float* __restrict__ ms,
-                                  const float* __restrict__ eps, const float* __restrict__ dzdec,
-                                  const float* __restrict__ draw, const float* __restrict__ colsq,
-                                  const float* __restrict__ coldot, int B, int L, int metric,
-                                  float w, float inv_bg, float* __restrict__ dhead, int ldh,
+// One thread per (pair b, W consecutive latent elements): the four backward rows from one
+// read of the three passes' mu / s and dz_dec; z and eps are recomputed exactly as the forward
+// produced them (reparam, eps_get), so neither is read from memory.
+template <bool V4>
+__global__ void latent_bwd_kernel(const float* __restrict__ ms, EpsSrc es,
+                                  const float* __restrict__ dzdec, const float* __restrict__ draw,
+                                  const float* __restrict__ colsq, const float* __restrict__ coldot,
+                                  int B, int L, int metric, float w, float inv_bg,
+                                  float* __restrict__ dhead, int ldh,
                                   unsigned short* __restrict__ hp, long long ps, int np) {
-  // one thread per (b, i): the four backward rows of element i of pair b from one read of its
-  // three z values, the lock mu/s and the rot/key s, the three eps and dz_dec
+  constexpr int W = V4 ? 4 : 1;
+  const int LW = L / W;
   const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= (size_t)B * L) return;
-  const int b = (int)(idx / L), i = (int)(idx - (size_t)b * L);
-  const float zr = z[(size_t)b * ldz + i];
-  const float zl = z[(size_t)(B + b) * ldz + i];
-  const float zk = z[(size_t)(2 * B + b) * ldz + i];
-  const float s_r = ms[(size_t)b * 2 * L + L + i];
-  const float mu_l = ms[(size_t)(B + b) * 2 * L + i];
-  const float s_l = ms[(size_t)(B + b) * 2 * L + L + i];
-  const float s_k = ms[(size_t)(2 * B + b) * 2 * L + L + i];
-  const float e_r = eps[((size_t)eps_slot(0) * B + b) * L + i];
-  const float e_l = eps[((size_t)eps_slot(1) * B + b) * L + i];
-  const float e_k = eps[((size_t)eps_slot(2) * B + b) * L + i];
-  const float ex_l = expf(s_l);
-  const float sig_r = sqrtf(expf(s_r)), sig_l = sqrtf(ex_l), sig_k = sqrtf(expf(s_k));
-  const float def = 2.f * w * (zl - zr) * inv_bg;
-  float dz2, dz3;  // g2 rows: lock, key
-  {
-    const float dr = draw[b];
+  if (idx >= (size_t)B * LW) return;
+  const int b = (int)(idx / LW), i = W * (int)(idx - (size_t)b * LW);
+  float mu[3][4], sg[3][4], e[3][4], dd[4];
+#pragma unroll
+  for (int blk = 0; blk < 3; ++blk) {
+    const float* row = ms + (size_t)(blk * B + b) * 2 * L;
+    if constexpr (V4) { ld4(row + i, mu[blk]); ld4(row + L + i, sg[blk]); }
+    else { mu[blk][0] = row[i]; sg[blk][0] = row[L + i]; }
+    eps_get<V4>(es, blk, b, i, B, L, e[blk]);
+  }
+  if constexpr (V4) ld4(dzdec + (size_t)b * L + i, dd);
+  else dd[0] = dzdec[(size_t)b * L + i];
+  const float dr = draw[b];
+  float out[4][2][4];  // [row q][dmu | ds][element]
+#pragma unroll
+  for (int j = 0; j < W; ++j) {
+    const float zr = reparam(mu[0][j], sg[0][j], e[0][j]);
+    const float zl = reparam(mu[1][j], sg[1][j], e[1][j]);
+    const float zk = reparam(mu[2][j], sg[2][j], e[2][j]);
+    const float ex_l = expf(sg[1][j]);
+    const float sig_r = sqrtf(expf(sg[0][j])), sig_l = sqrtf(ex_l), sig_k = sqrtf(expf(sg[2][j]));
+    const float def = 2.f * w * (zl - zr) * inv_bg;
+    float dz2, dz3;  // g2 rows: lock, key
     if (metric == 1) {
       dz2 = 2.f * dr * (zl - zk);
       dz3 = -dz2;
     } else {
-      const float ssl = colsq[i], ssk = colsq[L + i];
+      const float ssl = colsq[i + j], ssk = colsq[L + i + j];
       const float rl = rsqrtf(fmaxf(ssl, L2_EPS)), rk = rsqrtf(fmaxf(ssk, L2_EPS));
-      const float nl = zl * rl, nk = zk * rk, c = coldot[i];
+      const float nl = zl * rl, nk = zk * rk, c = coldot[i + j];
       dz2 = rl * (dr * nk - (ssl >= L2_EPS ? nl * c : 0.f));
       dz3 = rk * (dr * nl - (ssk >= L2_EPS ? nk * c : 0.f));
     }
+    const float dz1 = dd[j] + def;
+    out[0][0][j] = -def;
+    out[1][0][j] = dz1 + mu[1][j] * inv_bg;
+    out[2][0][j] = dz2;
+    out[3][0][j] = dz3;
+    out[0][1][j] = -0.5f * def * e[0][j] * sig_r;
+    out[1][1][j] = 0.5f * dz1 * e[1][j] * sig_l + 0.5f * (ex_l - 1.f) * inv_bg;
+    out[2][1][j] = 0.5f * dz2 * e[1][j] * sig_l;
+    out[3][1][j] = 0.5f * dz3 * e[2][j] * sig_k;
   }
-  const float dz1 = dzdec[(size_t)b * L + i] + def;
-  const float dmu[4] = {-def, dz1 + mu_l * inv_bg, dz2, dz3};
-  const float ds[4] = {-0.5f * def * e_r * sig_r, 0.5f * dz1 * e_l * sig_l + 0.5f * (ex_l - 1.f) * inv_bg,
-                       0.5f * dz2 * e_l * sig_l, 0.5f * dz3 * e_k * sig_k};
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const size_t o = (size_t)(q * B + b) * ldh;
-    if (dhead) {
-      dhead[o + i] = dmu[q];
-      dhead[o + L + i] = ds[q];
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const size_t o = (size_t)(q * B + b) * ldh + h * L + i;
+      if constexpr (V4) {
+        if (dhead) *reinterpret_cast<float4*>(dhead + o) = make_float4(out[q][h][0], out[q][h][1], out[q][h][2], out[q][h][3]);
+        if (hp) planes_put4(hp, ps, np, o, out[q][h]);
+      } else {
+        if (dhead) dhead[o] = out[q][h][0];
+        if (hp) planes_put(hp, ps, np, o, out[q][h][0]);
+      }
     }
-    if (hp) {
-      planes_put(hp, ps, np, o + i, dmu[q]);
-      planes_put(hp, ps, np, o + L + i, ds[q]);
-    }
-  }
 }
 
 // ---------------------------------------------------------------- dual TF-Adam
@@ -540,17 +646,29 @@ hipError_t launch_normal(float* out, int slots, int B, int L, int Bg, int off, u
   return hipGetLastError();
 }
 
-hipError_t launch_latent_fwd(const float* ms, const float* eps, float* z, const Planes& zp, int B,
-                             int L, int ldz, hipStream_t st) {
-  if (L % 4 == 0 && ldz % 4 == 0) {
-    const size_t n4 = (size_t)3 * B * (L / 4);
-    hipLaunchKernelGGL(latent_fwd4_kernel, dim3(nblocks(n4, 256)), dim3(256), 0, st, ms, eps, z, zp.p,
-                       zp.stride, zp.n, B, L, ldz);
-    return hipGetLastError();
-  }
-  const size_t n = (size_t)3 * B * L;
-  hipLaunchKernelGGL(latent_fwd_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, ms, eps, z, zp.p,
-                     zp.stride, zp.n, B, L, ldz);
+static EpsSrc eps_src(const LatentEps& le) {
+  EpsSrc es;
+  es.buf = le.buf;
+  es.seed = le.seed;
+  es.counter = le.counter;
+  es.Bg = le.Bg;
+  es.off = le.off;
+  return es;
+}
+
+hipError_t launch_latent_fwd(const float* ms, const LatentEps& le, float* z, const Planes& zp,
+                             int zmask, int B, int L, int ldz, float* rowfwd, hipStream_t st) {
+  const EpsSrc es = eps_src(le);
+  const bool v4 = L % 4 == 0 && ldz % 4 == 0;
+  if (v4 && L >= 1024)
+    hipLaunchKernelGGL((latent_fwd_kernel<true, 4>), dim3(B), dim3(256), 0, st, ms, es, z, zp.p,
+                       zp.stride, zp.n, zmask, B, L, ldz, rowfwd);
+  else if (v4)
+    hipLaunchKernelGGL((latent_fwd_kernel<true, 1>), dim3(nblocks(B, 4)), dim3(256), 0, st, ms, es, z,
+                       zp.p, zp.stride, zp.n, zmask, B, L, ldz, rowfwd);
+  else
+    hipLaunchKernelGGL((latent_fwd_kernel<false, 1>), dim3(nblocks(B, 4)), dim3(256), 0, st, ms, es, z,
+                       zp.p, zp.stride, zp.n, zmask, B, L, ldz, rowfwd);
   return hipGetLastError();
 }
 
@@ -565,11 +683,11 @@ hipError_t launch_colstats(int mode, const float* z, int B, int L, int ldz, cons
   return hipGetLastError();
 }
 
-hipError_t launch_metric(const float* z, int ldz, const float* ms, const float* rowpart, int nblk,
+hipError_t launch_metric(const float* z, int ldz, const float* rowfwd, const float* rowpart, int nblk,
                          const float* areas, const float* colsq, int B, int L, int metric, int recip,
                          float w, float inv_bg, float* rowvals, float* dist, float* draw,
                          hipStream_t st) {
-  hipLaunchKernelGGL(metric_kernel, dim3(nblocks(B, 4)), dim3(256), 0, st, z, ldz, ms, rowpart, nblk,
+  hipLaunchKernelGGL(metric_kernel, dim3(nblocks(B, 4)), dim3(256), 0, st, z, ldz, rowfwd, rowpart, nblk,
                      areas, colsq, B, L, metric, recip, w, inv_bg, rowvals, dist, draw);
   return hipGetLastError();
 }
@@ -579,13 +697,19 @@ hipError_t launch_loss_reduce(const float* rowvals, int B, float inv_bg, float* 
   return hipGetLastError();
 }
 
-hipError_t launch_latent_bwd(const float* z, int ldz, const float* ms, const float* eps,
-                             const float* dzdec, const float* draw, const float* colsq,
-                             const float* coldot, int B, int L, int metric, float w, float inv_bg,
-                             float* dhead, int ldh, const Planes& hp, hipStream_t st) {
-  const size_t n = (size_t)B * L;
-  hipLaunchKernelGGL(latent_bwd_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, z, ldz, ms, eps, dzdec,
-                     draw, colsq, coldot, B, L, metric, w, inv_bg, dhead, ldh, hp.p, hp.stride, hp.n);
+hipError_t launch_latent_bwd(const float* ms, const LatentEps& le, const float* dzdec, const float* draw,
+                             const float* colsq, const float* coldot, int B, int L, int metric, float w,
+                             float inv_bg, float* dhead, int ldh, const Planes& hp, hipStream_t st) {
+  const EpsSrc es = eps_src(le);
+  if (L % 4 == 0 && ldh % 4 == 0) {
+    const size_t n = (size_t)B * (L / 4);
+    hipLaunchKernelGGL(latent_bwd_kernel<true>, dim3(nblocks(n, 256)), dim3(256), 0, st, ms, es, dzdec,
+                       draw, colsq, coldot, B, L, metric, w, inv_bg, dhead, ldh, hp.p, hp.stride, hp.n);
+  } else {
+    const size_t n = (size_t)B * L;
+    hipLaunchKernelGGL(latent_bwd_kernel<false>, dim3(nblocks(n, 256)), dim3(256), 0, st, ms, es, dzdec,
+                       draw, colsq, coldot, B, L, metric, w, inv_bg, dhead, ldh, hp.p, hp.stride, hp.n);
+  }
   return hipGetLastError();
 }
 

@@ -22,12 +22,12 @@ def rows(d, suffix):
     return out
 
 
-def short(name, full):
+def short(name, full, grid=None):
     if full:
         return name
-    n = re.sub(r"^void ", "", name)
-    n = re.sub(r"\(.*$", "", n)
-    return n
+    n = re.sub(r"^void ", "", name).replace("mvae::(anonymous namespace)::", "")
+    n = n[:n.index("(")] if "(" in n else n
+    return n + (f" grid={grid}" if grid else "")
 
 
 def main():
@@ -47,7 +47,7 @@ def main():
                 continue
             did = int(r["Dispatch_Id"])
             per[did][r["Counter_Name"]] += float(r["Counter_Value"])
-            names[did] = short(k, args.full)
+            names[did] = short(k, args.full, r.get("Grid_Size"))
         for did, cs in per.items():
             for c, v in cs.items():
                 val[names[did]][c].append(v)
@@ -55,7 +55,7 @@ def main():
             k = r["Kernel_Name"]
             if args.match and args.match not in k:
                 continue
-            dur[short(k, args.full)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+            dur[short(k, args.full, r.get("Grid_Size"))].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     for k in sorted(set(val) | set(dur)):
         print(k)
         if dur.get(k):
