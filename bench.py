@@ -69,6 +69,9 @@ def parse_args(argv=None):
     ap.add_argument("--pmc-child", default="", help=argparse.SUPPRESS)
     ap.add_argument("--opt", action="append", default=[],
                     help="libmvae schedule switch NAME=VALUE (mvae_set_option), repeatable")
+    ap.add_argument("--no-configs", action="store_true",
+                    help="skip the configs block (C3 / C5 on one GPU; C4 / C5 with N ranks)")
+    ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive h2d leg")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launcher / data-parallel / timing / JSON path "
                          "(gloo, a stand-in engine; no GPU, no kernels, not a measurement)")
@@ -459,45 +462,18 @@ def dry_run_batch(cfg, world, rank, j):
     return X[rank * B:(rank + 1) * B].contiguous(), A[rank * B:(rank + 1) * B].contiguous()
 
 
-# ------------------------------------------------------------------------ main
-def main():
-    argv = sys.argv[1:]
-    args = parse_args(argv)
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(self_launch(args, argv))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-
+# ------------------------------------------------------------------------ measurement
+def measure(args, cfg, world, rank, local, dev, *, timing, steps, warmup, keep=False, h2d=False):
+    """One configuration through the training step: W warm-up steps, a region pass (HIP events
+    around every region, outside the timed loop), K timed steps bracketed by barrier + device
+    sync (max over ranks), overlap-MSE on a held-out batch. h2d: a further timed loop in which
+    every step's X first comes from pinned host memory (copied on a side stream one step ahead,
+    mirroring feed_dict, 11a/vae.py:399-402). Returns a dict; the engine stays open with keep."""
     import torch
     import torch.distributed as dist
 
     from magic_amd import _lib
-    from magic_amd.config import baseline_config
     from magic_amd.parallel import DataParallelStep
-
-    if world != args.gpus:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    if args.dry_run:
-        dev = torch.device("cpu")
-    else:
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
-    if world > 1:
-        if args.dry_run:
-            dist.init_process_group("gloo")
-        else:
-            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
-        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
-
-    cfg = baseline_config(args.config)
-    if args.batch:
-        cfg = cfg.replace(batch=args.batch)
-    if args.precision:
-        cfg = cfg.replace(precision=args.precision)
-    # one seed on every rank: each rank's internal sampler draws its own rows of the global
-    # batch's eps stream (Engine.set_shard via DataParallelStep)
-    cfg = cfg.replace(global_batch=cfg.batch * world)
 
     if args.dry_run:
         eng = DryRunEngine(cfg)
@@ -514,23 +490,12 @@ def main():
                 for j in range(2)]
         torch.cuda.synchronize()
     stepper = DataParallelStep(eng, reduce_losses=True)
-    timing = not (args.no_timing or args.dry_run or args.pmc_child)
 
     def sync():
         if not args.dry_run:
             torch.cuda.synchronize()
 
-    if args.pmc_child:  # profiler child: markers around the named regions, a few steps
-        names = eng.timing_names()
-        for rid in args.pmc_child.split(","):
-            eng.timing_marker(names[int(rid)], True)
-        for i in range(args.warmup + args.steps):
-            stepper.step(*pool[i % 2])
-        sync()
-        eng.close()
-        return
-
-    for i in range(args.warmup):
+    for i in range(warmup):
         stepper.step(*pool[i % 2])
     sync()
     regions, dom = {}, None
@@ -554,127 +519,291 @@ def main():
         eng.timing_reset()
         eng.timing_select(dom)
         eng.timing_enable(True)
-    if world > 1:
-        dist.barrier()
-    sync()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        stepper.step(*pool[i % 2])
-    if world > 1:
-        dist.barrier()
-    sync()
-    elapsed = time.perf_counter() - t0
+
+    def timed(n, batch_of):
+        if world > 1:
+            dist.barrier()
+        sync()
+        t0 = time.perf_counter()
+        for i in range(n):
+            stepper.step(*batch_of(i))
+        if world > 1:
+            dist.barrier()
+        sync()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    elapsed = timed(steps, lambda i: pool[i % 2])
     dom_timed = None
     if timing:
         eng.timing_enable(False)
         dom_timed = eng.timing_read().get(dom)
         eng.timing_select(None)
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     losses = eng.losses.cpu().numpy().tolist()
     if not np.all(np.isfinite(losses)):
         raise RuntimeError(f"non-finite losses after the timed steps: {losses}")
+    out = {"cfg": cfg, "elapsed": elapsed, "steps": steps, "regions": regions, "dom": dom,
+           "dom_timed": dom_timed, "losses": losses}
+    if not args.dry_run:
+        out["n_all"] = eng.buffer(_lib.BUF_PARAMS).numel()
+        out["n_enc"] = eng.buffer(_lib.BUF_GRADS).numel() - out["n_all"]
+        if cfg.precision == "f32x":
+            out["dyn"] = int(eng.buffer(_lib.BUF_DYN).view(torch.int32).item())
+    if h2d and not args.dry_run:
+        # X of every step from pinned host memory: the copy of step i+1's batch runs on a copy
+        # stream beside step i (two device buffers), as an input pipeline feeding the step would
+        host = [pool[j][0].cpu().pin_memory() for j in range(2)]
+        bufs = [torch.empty_like(pool[0][0]) for _ in range(2)]
+        cs = torch.cuda.Stream(device=dev)
+        ev = [torch.cuda.Event() for _ in range(2)]
 
+        def fetch(i):
+            with torch.cuda.stream(cs):
+                bufs[i % 2].copy_(host[i % 2], non_blocking=True)
+                ev[i % 2].record(cs)
+        fetch(0)
+
+        def batch_h2d(i):
+            torch.cuda.current_stream().wait_event(ev[i % 2])
+            if i + 1 < steps:
+                cs.wait_stream(torch.cuda.current_stream())  # buffer (i+1)%2 no longer read
+                fetch(i + 1)
+            return bufs[i % 2], pool[i % 2][1]
+        el_h = timed(steps, batch_h2d)
+        out["h2d"] = {"value": round(cfg.batch * world * steps / el_h, 2), "unit": "shape-pairs/s",
+                      "ms_per_step": round(el_h / steps * 1e3, 4),
+                      "bytes_per_step": int(pool[0][0].numel() * 4),
+                      "note": "PCIe-inclusive: each step's X [B, 3D] f32 copied pinned host -> HBM "
+                              "(one step ahead on a copy stream), mirroring feed_dict "
+                              "(11a/vae.py:399-402); never the headline value"}
     # overlap-MSE on a held-out seeded batch (11a/main.py:94-111; 1/pred for reciprocal)
     if args.dry_run:
         xe, ae = dry_run_batch(cfg, world, rank, 99)
     else:
+        from magic_amd.overlap_input import synthetic_batch
         xe, ae = synthetic_batch(cfg.batch, cfg.image_size, seed=999, device=dev)
     pred = stepper.predict(xe).double()   # global-batch cosine norms under DP
     if cfg.reciprocal:
         pred = 1.0 / pred
-    mse = float(((pred - ae.double()) ** 2).mean().item())
+    out["mse"] = float(((pred - ae.double()) ** 2).mean().item())
+    if args.dry_run:
+        w = torch.arange(1, eng.grads.numel() + 1, dtype=torch.float64)
+        out["grad_checksum"] = float((eng.grads * w).sum())
+    if keep:
+        out["eng"] = eng
+    else:
+        eng.close()
+    return out
+
+
+def rooflines(args, m):
+    """roofline (dominant GEMM) and loss_roofline (HBM-bound kernels) of one measured config."""
+    cfg, regions, dom, dom_timed = m["cfg"], m["regions"], m["dom"], m["dom_timed"]
+    if not regions or not dom_timed:
+        return None, None
+    gemms = {k: v for k, v in regions.items() if region_flops(cfg, k) > 0}
+    # per step (a region may be several launches: the layer-0 weight gradient in row chunks)
+    ms_avg = dom_timed[0] / m["steps"]  # HIP events over the timed loop
+    flops = region_flops(cfg, dom)
+    achieved = flops / (ms_avg * 1e-3) / 1e12
+    peak = F32_MFMA_PEAK_TFLOPS if cfg.precision == "f32" else BF16_MFMA_PEAK_TFLOPS
+    iso_ms = regions[dom][0] / args.region_steps
+    roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
+                "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
+                "kernel": dom, "flops_per_launch": flops, "avg_ms": round(ms_avg, 4),
+                "isolated_avg_ms": round(iso_ms, 4),
+                "isolated_frac": round(flops / (iso_ms * 1e-3) / 1e12 / peak, 4),
+                "work": "algorithmic 2*M*N*K of the region's fp32 GEMM, counted once"}
+    if cfg.precision == "f32x":
+        pp = plane_pairs(cfg, dom, m.get("dyn", 0) == 0)
+        roofline.update({
+            "arith": "f32x: fp32-accurate exact 3-term bf16 split on the bf16 MFMA pipe",
+            "bf16_plane_pairs": pp,
+            "mfma_pipe_tflops": round(achieved * pp, 2),
+            "mfma_pipe_frac": round(achieved * pp / BF16_MFMA_PEAK_TFLOPS, 4),
+            "frac_of_fp32_mfma_peak": round(achieved / F32_MFMA_PEAK_TFLOPS, 4)})
+    rs = args.region_steps
+    total_gemm_ms = sum(v[0] for v in gemms.values()) / rs
+    gemm_flops = sum(region_flops(cfg, k) * v[1] for k, v in gemms.items()) / rs
+    roofline["all_gemms"] = {"ms_per_step": round(total_gemm_ms, 4),
+                             "tflops": round(gemm_flops / total_gemm_ms / 1e9, 2)}
+    # HBM-bound kernels and the fused BCE head (north_star: achieved GB/s vs peak)
+    loss_roofline = {}
+    np_ = {"f32": 0, "bf16": 1, "f32x": 3}[cfg.precision]
+    for k in ("deinterleave", "eps_rng", "latent_fwd", "colsq", "metric_loss", "coldot",
+              "latent_bwd", "adam", "conv1_fwd", "lrn2_pool2_fwd", "pool2_bwd", "conv1_wgrad"):
+        if k not in regions:
+            continue
+        ms_k = regions[k][0] / args.region_steps
+        by = adam_bytes(m["n_all"], m["n_enc"], np_) if k == "adam" else region_bytes(cfg, k)
+        loss_roofline[k] = {"bytes": by, "avg_ms": round(ms_k, 4),
+                            "gbs": round(by / (ms_k * 1e-3) / 1e9, 1),
+                            "frac": round(by / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    lat = [k for k in ("eps_rng", "latent_fwd", "colsq", "metric_loss", "coldot", "latent_bwd")
+           if k in regions]
+    ms_lat = sum(regions[k][0] / args.region_steps for k in lat)
+    by_lat = 80.0 * cfg.latent * cfg.batch
+    loss_roofline["latent_head_total"] = {
+        "kernels": lat, "avg_ms": round(ms_lat, 4), "bytes_survey": by_lat,
+        "gbs_survey": round(by_lat / (ms_lat * 1e-3) / 1e9, 1),
+        "frac_survey": round(by_lat / (ms_lat * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "note": "SURVEY.md §8d: ~80*L B/pair for the fused latent head fwd+bwd"}
+    if "dec_fwd_out_bce" in regions:
+        ms_b = regions["dec_fwd_out_bce"][0] / args.region_steps
+        by_b = 12.0 * cfg.D * cfg.batch
+        loss_roofline["bce_head"] = {
+            "bytes": by_b, "avg_ms": round(ms_b, 4),
+            "gbs": round(by_b / (ms_b * 1e-3) / 1e9, 1),
+            "frac": round(by_b / (ms_b * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "note": "BASELINE.md §4: 12*D B/pair (logits, targets, dlogits); fused into the "
+                    "decoder-output GEMM epilogue, whose time is MFMA-bound"}
+    return roofline, loss_roofline
+
+
+def print_regions(args, m, tag):
+    cfg, regions, dom = m["cfg"], m["regions"], m["dom"]
+    if not regions:
+        return
+    gemms = {k: v for k, v in regions.items() if region_flops(cfg, k) > 0}
+    rs = args.region_steps
+    total_gemm_ms = sum(v[0] for v in gemms.values()) / rs
+    gemm_flops = sum(region_flops(cfg, k) * v[1] for k, v in gemms.items()) / rs
+    ms_dom = m["dom_timed"][0] / m["steps"] if m["dom_timed"] else float("nan")
+    print(f"[bench] {tag}: region pass ({rs} steps, kernels serialised on one stream): GEMM time/step "
+          f"{total_gemm_ms:.3f} ms, {gemm_flops / total_gemm_ms / 1e9:.1f} TFLOP/s over all GEMMs; timed step "
+          f"{m['elapsed'] / m['steps'] * 1e3:.3f} ms; {dom} {ms_dom:.4f} ms in the timed loop", file=sys.stderr)
+    _, lr = rooflines(args, m)
+    for k, (ms, n) in sorted(regions.items(), key=lambda kv: -kv[1][0]):
+        fl = region_flops(cfg, k)
+        extra = f"  {fl / (ms / rs * 1e-3) / 1e12:7.1f} TF/s" if fl else ""
+        if lr and k in lr:
+            extra = f"  {lr[k]['gbs']:7.1f} GB/s"
+        print(f"[bench] {k:18s} {ms / rs:9.4f} ms/step ({n} launches){extra}", file=sys.stderr)
+
+
+def workload(args_config, cfg):
+    return (f"BASELINE {args_config}: "
+            f"{'CifarNet conv tower (6b/net.py:50-60) + ' if cfg.conv else ''}preset "
+            f"{ {20: '8c', 200: '8d', 2000: '8e'}.get(cfg.latent, '?') } enc "
+            f"{list(cfg.enc)} L={cfg.latent} {cfg.act} "
+            f"{'reciprocal ' if cfg.reciprocal else ''}{cfg.metric}")
+
+
+# ------------------------------------------------------------------------ main
+def main():
+    argv = sys.argv[1:]
+    args = parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args, argv))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+    import torch.distributed as dist
+
+    from magic_amd import _lib
+    from magic_amd.config import baseline_config
+
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.dry_run:
+        dev = torch.device("cpu")
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    if world > 1:
+        if args.dry_run:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)  # RCCL over xGMI
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
+
+    def config_of(cid, batch=0, precision="", small=False):
+        cfg = baseline_config(cid)
+        if batch:
+            cfg = cfg.replace(batch=batch)
+        if precision:
+            cfg = cfg.replace(precision=precision)
+        if small:  # launcher rehearsal of the configs block: a small stand-in shape
+            cfg = cfg.replace(batch=min(cfg.batch, 16), image_size=12, latent=min(cfg.latent, 16))
+        # one seed on every rank: each rank's internal sampler draws its own rows of the global
+        # batch's eps stream (Engine.set_shard via DataParallelStep)
+        return cfg.replace(global_batch=cfg.batch * world)
+
+    cfg = config_of(args.config, args.batch, args.precision)
+    timing = not (args.no_timing or args.dry_run or args.pmc_child)
+
+    if args.pmc_child:  # profiler child: markers around the named regions, a few steps
+        from magic_amd.engine import Engine
+        from magic_amd.overlap_input import synthetic_batch
+        from magic_amd.parallel import DataParallelStep
+        eng = Engine(cfg, local)
+        eng.init_params(0)
+        pool = [synthetic_batch(cfg.batch, cfg.image_size, seed=17 + j, device=dev) for j in range(2)]
+        stepper = DataParallelStep(eng, reduce_losses=True)
+        names = eng.timing_names()
+        for rid in args.pmc_child.split(","):
+            eng.timing_marker(names[int(rid)], True)
+        for i in range(args.warmup + args.steps):
+            stepper.step(*pool[i % 2])
+        torch.cuda.synchronize()
+        eng.close()
+        return
+
+    head = measure(args, cfg, world, rank, local, dev, timing=timing, steps=args.steps,
+                   warmup=args.warmup, keep=True, h2d=not args.no_h2d)
+    eng = head.pop("eng")
+    if rank == 0:
+        print_regions(args, head, f"{args.config}")
+    # the other BASELINE configurations in the same run (their own rooflines): C3 (the
+    # north_star's L = 200 target) and C5 (L = 2000) on one GPU; with N ranks, C4 (= C3's shape
+    # per rank, global batch 8192 N) and C5 at N ranks
+    extra = {}
+    if not args.no_configs:
+        ids = ["C3", "C5"] if world == 1 else ["C4", "C5"]
+        for cid in ids:
+            if cid == args.config or (cid == "C4" and args.config == "C3"):
+                continue
+            c = config_of("C3" if cid == "C4" else cid, small=args.dry_run)
+            m = measure(args, c, world, rank, local, dev, timing=timing, steps=args.steps,
+                        warmup=args.warmup)
+            if rank == 0:
+                print_regions(args, m, cid)
+                rf, lr = rooflines(args, m)
+                extra[cid] = {"workload": workload("C3" if cid == "C4" else cid, c) +
+                              (f" x {world} ranks" if world > 1 else ""),
+                              "value": round(c.batch * world * m["steps"] / m["elapsed"], 2),
+                              "unit": "shape-pairs/s", "per_gpu_value": round(c.batch * m["steps"] / m["elapsed"], 2),
+                              "ms_per_step": round(m["elapsed"] / m["steps"] * 1e3, 4),
+                              "global_batch": c.batch * world, "per_gpu_batch": c.batch,
+                              "dtype": c.precision, "overlap_mse": round(m["mse"], 2),
+                              "roofline": rf, "loss_roofline": lr}
 
     if rank == 0:
         pairs = cfg.batch * world * args.steps
-        value = pairs / elapsed
-        roofline, loss_roofline = None, None
-        if regions and dom_timed:
-            gemms = {k: v for k, v in regions.items() if region_flops(cfg, k) > 0}
-            ms_avg = dom_timed[0] / dom_timed[1]  # HIP events over the timed loop
-            flops = region_flops(cfg, dom)
-            achieved = flops / (ms_avg * 1e-3) / 1e12
-            peak = F32_MFMA_PEAK_TFLOPS if cfg.precision == "f32" else BF16_MFMA_PEAK_TFLOPS
-            iso_ms = regions[dom][0] / regions[dom][1]
-            roofline = {"bound": "mfma", "achieved": round(achieved, 2), "peak": peak,
-                        "unit": "TFLOP/s", "frac": round(achieved / peak, 4), "traffic": None,
-                        "kernel": dom, "flops_per_launch": flops, "avg_ms": round(ms_avg, 4),
-                        "isolated_avg_ms": round(iso_ms, 4),
-                        "isolated_frac": round(flops / (iso_ms * 1e-3) / 1e12 / peak, 4),
-                        "work": "algorithmic 2*M*N*K of the region's fp32 GEMM, counted once"}
-            if cfg.precision == "f32x":
-                dyn = int(eng.buffer(_lib.BUF_DYN).view(torch.int32).item())
-                pp = plane_pairs(cfg, dom, dyn == 0)
-                roofline.update({
-                    "arith": "f32x: fp32-accurate exact 3-term bf16 split on the bf16 MFMA pipe",
-                    "bf16_plane_pairs": pp,
-                    "mfma_pipe_tflops": round(achieved * pp, 2),
-                    "mfma_pipe_frac": round(achieved * pp / BF16_MFMA_PEAK_TFLOPS, 4),
-                    "frac_of_fp32_mfma_peak": round(achieved / F32_MFMA_PEAK_TFLOPS, 4)})
-            rs = args.region_steps
-            total_gemm_ms = sum(v[0] for v in gemms.values()) / rs
-            gemm_flops = sum(region_flops(cfg, k) * v[1] for k, v in gemms.items()) / rs
-            roofline["all_gemms"] = {"ms_per_step": round(total_gemm_ms, 4),
-                                     "tflops": round(gemm_flops / total_gemm_ms / 1e9, 2)}
-            # HBM-bound kernels and the fused BCE head (north_star: achieved GB/s vs peak)
-            loss_roofline = {}
-            n_all = eng.buffer(_lib.BUF_PARAMS).numel()
-            n_enc = eng.buffer(_lib.BUF_GRADS).numel() - n_all
-            np_ = {"f32": 0, "bf16": 1, "f32x": 3}[cfg.precision]
-            for k in ("deinterleave", "eps_rng", "latent_fwd", "colsq", "metric_loss", "coldot",
-                      "latent_bwd", "adam", "conv1_fwd", "lrn2_pool2_fwd", "pool2_bwd", "conv1_wgrad"):
-                if k not in regions:
-                    continue
-                ms_k = regions[k][0] / regions[k][1]
-                by = adam_bytes(n_all, n_enc, np_) if k == "adam" else region_bytes(cfg, k)
-                loss_roofline[k] = {"bytes": by, "avg_ms": round(ms_k, 4),
-                                    "gbs": round(by / (ms_k * 1e-3) / 1e9, 1),
-                                    "frac": round(by / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-            lat = [k for k in ("eps_rng", "latent_fwd", "colsq", "metric_loss", "coldot", "latent_bwd")
-                   if k in regions]
-            ms_lat = sum(regions[k][0] / regions[k][1] for k in lat)
-            by_lat = 80.0 * cfg.latent * cfg.batch
-            loss_roofline["latent_head_total"] = {
-                "kernels": lat, "avg_ms": round(ms_lat, 4), "bytes_survey": by_lat,
-                "gbs_survey": round(by_lat / (ms_lat * 1e-3) / 1e9, 1),
-                "frac_survey": round(by_lat / (ms_lat * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "note": "SURVEY.md §8d: ~80*L B/pair for the fused latent head fwd+bwd"}
-            if "dec_fwd_out_bce" in regions:
-                ms_b = regions["dec_fwd_out_bce"][0] / regions["dec_fwd_out_bce"][1]
-                by_b = 12.0 * cfg.D * cfg.batch
-                loss_roofline["bce_head"] = {
-                    "bytes": by_b, "avg_ms": round(ms_b, 4),
-                    "gbs": round(by_b / (ms_b * 1e-3) / 1e9, 1),
-                    "frac": round(by_b / (ms_b * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                    "note": "BASELINE.md §4: 12*D B/pair (logits, targets, dlogits); fused into the "
-                            "decoder-output GEMM epilogue, whose time is MFMA-bound"}
-            print(f"[bench] region pass ({rs} steps, kernels serialised on one stream): GEMM time/step {total_gemm_ms:.3f} ms, "
-                  f"{gemm_flops / total_gemm_ms / 1e9:.1f} TFLOP/s over all GEMMs; timed step "
-                  f"{elapsed / args.steps * 1e3:.3f} ms; {dom} {ms_avg:.4f} ms in the timed loop",
-                  file=sys.stderr)
-            for k, (ms, n) in sorted(regions.items(), key=lambda kv: -kv[1][0]):
-                fl = region_flops(cfg, k)
-                extra = f"  {fl / (ms / n * 1e-3) / 1e12:7.1f} TF/s" if fl else ""
-                if k in loss_roofline:
-                    extra = f"  {loss_roofline[k]['gbs']:7.1f} GB/s"
-                print(f"[bench] {k:18s} {ms / n:9.4f} ms x{n}{extra}", file=sys.stderr)
+        value = pairs / head["elapsed"]
+        roofline, loss_roofline = rooflines(args, head)
         cpu = None
         if world == 1 and not args.no_cpu_baseline and not args.dry_run:
             cpu = cpu_baseline(cfg, dev, args.cpu_seconds)
         if roofline and world == 1 and args.pmc == "auto" and not args.dry_run:
             names = eng.timing_names()
-            want = [dom] + [k for k in PMC_REGIONS_BW if k in regions]
+            want = [head["dom"]] + [k for k in PMC_REGIONS_BW if k in head["regions"]]
             tr, how = pmc_traffic(args, want, names)
             roofline["traffic_method"] = how
             if tr:
-                if dom in tr:
-                    roofline["traffic"] = tr[dom]["hbm_bytes"]
-                    roofline["traffic_detail"] = tr[dom]
+                if head["dom"] in tr:
+                    roofline["traffic"] = tr[head["dom"]]["hbm_bytes"]
+                    roofline["traffic_detail"] = tr[head["dom"]]
                 for k in PMC_REGIONS_BW:
                     if k in tr and k in loss_roofline:
                         loss_roofline[k]["traffic"] = tr[k]["hbm_bytes"]
+        losses = head["losses"]
         line = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -682,7 +811,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(head["elapsed"] / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -693,26 +822,24 @@ def main():
                      "synthetic 100x100 binary shape pairs (random ellipses/rectangles, nearest-"
                      "neighbour rotated lock), areas resampled from the reference's OVERLAP_AREAS; "
                      "random xavier init"),
-            "config": {"workload": f"BASELINE {args.config}: "
-                                   f"{'CifarNet conv tower (6b/net.py:50-60) + ' if cfg.conv else ''}preset "
-                                   f"{ {20: '8c', 200: '8d', 2000: '8e'}.get(cfg.latent, '?') } enc "
-                                   f"{list(cfg.enc)} L={cfg.latent} {cfg.act} "
-                                   f"{'reciprocal ' if cfg.reciprocal else ''}{cfg.metric}",
+            "config": {"workload": workload(args.config, cfg),
                        "global_batch": cfg.batch * world, "per_gpu_batch": cfg.batch,
                        "image": f"{cfg.image_size}x{cfg.image_size}", "parallelism": f"dp{world}",
                        "collective": ("gloo (dry run)" if args.dry_run else "RCCL all-reduce")
                        if world > 1 else None},
             "per_gpu_value": round(value / world, 2),
-            "overlap_mse": round(mse, 2),
+            "overlap_mse": round(head["mse"], 2),
             "losses": {"cost": losses[0], "training_loss": losses[1], "r_l": losses[2],
                        "l_l": losses[3], "d_l": losses[4]},
             "roofline": roofline,
             "loss_roofline": loss_roofline,
             "cpu_baseline": cpu,
+            "h2d": head.get("h2d"),
+            "configs": extra,
+            "build_id": None if args.dry_run else _lib.load().mvae_build_id().decode(),
         }
         if args.dry_run:
-            w = torch.arange(1, eng.grads.numel() + 1, dtype=torch.float64)
-            line["grad_checksum"] = float((eng.grads * w).sum())
+            line["grad_checksum"] = head["grad_checksum"]
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:

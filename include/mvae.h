@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define MVAE_ABI_VERSION 3
+#define MVAE_ABI_VERSION 4
 #define MVAE_MAX_ENC 8
 
 enum { MVAE_OK = 0, MVAE_EINVAL = -1, MVAE_ECONFIG = -2, MVAE_ESTATE = -3 };
@@ -147,15 +147,20 @@ int mvae_forward(mvae_ctx* ctx, const float* x, const float* eps, void* stream);
 int mvae_metric(mvae_ctx* ctx, const float* areas, void* stream);
 /* Needs MVAE_BUF_COLDOT summed over ranks (cosine). Writes MVAE_BUF_GRADS.           */
 int mvae_backward(mvae_ctx* ctx, void* stream);
-/* The same backward in three parts (0: decoder; 1: latent head, encoder dgrad chain and
- * the layer-0 weight gradient; 2: the remaining encoder weight gradients). After part k,
- * the ranges mvae_grad_range(ctx, k, i = 0, 1, ...) are final: a data-parallel host
- * all-reduces them while the later parts run (returns MVAE_EINVAL past the last range). */
+/* The same backward in mvae_backward_nparts(ctx) = R + 2 parts, R = option "wgrad0_chunks"
+ * (0: decoder; 1: latent head, encoder dgrad chain and layer-0 weight-gradient chunk 0;
+ * 2 .. R: layer-0 chunks 1 .. R-1; R + 1: the remaining encoder weight gradients). After
+ * part k the ranges mvae_grad_range(ctx, k, i = 0, 1, ...) are final: a data-parallel host
+ * all-reduces them while the later parts run (returns MVAE_EINVAL past the last range). Over
+ * all parts the ranges cover MVAE_BUF_GRADS exactly once. */
+int mvae_backward_nparts(mvae_ctx* ctx);
 int mvae_backward_part(mvae_ctx* ctx, int part, void* stream);
 int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* count);
-/* Schedule switches (A/B measurement): "side_stream" (default 1) runs the weight gradients
- * on a context-owned side stream beside the dgrad chain, joined before the gradients they
- * write are reported final (mvae_backward / the end of each mvae_backward_part). */
+/* Schedule switches: "side_stream" (default 1) runs the weight gradients on a context-owned
+ * side stream beside the dgrad chain, joined before the gradients they write are reported
+ * final (mvae_backward / the end of each mvae_backward_part); "wgrad0_chunks" (1, 2, 4, 8;
+ * default 1) splits the layer-0 weight gradient (40 MB of the 69 MB bucket at C4) into row
+ * chunks that finish -- and can be all-reduced -- one after another. */
 int mvae_set_option(mvae_ctx* ctx, const char* name, int value);
 /* Both TF ApplyAdam updates from MVAE_BUF_GRADS (theta -= d1(g1) + d2(g2)).           */
 int mvae_adam(mvae_ctx* ctx, void* stream);

@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("MVAE_LIB", os.path.join(HERE, "libmvae.so"))
 
 MVAE_MAX_ENC = 8
 MARKER_GRID = 4096   # mvae_region_marker workgroups = MARKER_GRID + region (mvae_internal.h)
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 ACT = {"tanh": 0, "elu": 1}
 METRIC = {"cosine": 0, "sqdiff": 1}
@@ -70,6 +70,7 @@ _SIGS = {
     "mvae_metric": ([C.c_void_p, C.c_void_p, C.c_void_p], C.c_int),
     "mvae_backward": ([C.c_void_p, C.c_void_p], C.c_int),
     "mvae_backward_part": ([C.c_void_p, C.c_int, C.c_void_p], C.c_int),
+    "mvae_backward_nparts": ([C.c_void_p], C.c_int),
     "mvae_grad_range": ([C.c_void_p, C.c_int, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)], C.c_int),
     "mvae_set_option": ([C.c_void_p, C.c_char_p, C.c_int], C.c_int),
     "mvae_adam": ([C.c_void_p, C.c_void_p], C.c_int),

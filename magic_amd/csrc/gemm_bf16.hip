@@ -20,6 +20,7 @@
 #include "gemm_common.h"
 
 #include <cmath>
+#include <cstdlib>
 #include <cstdint>
 
 namespace mvae {
@@ -51,7 +52,15 @@ struct PParams {
   const int* dyn;                   // A residual planes nonzero? (nullptr: use all pairs)
   int diag;                         // timing diagnostics: bit 0 = no operand copies after the
                                     // prologue (the k-loop multiplies stale LDS images)
+  unsigned long long* stamps;       // twin kernel diagnostics build (ST): 4 stamps per workgroup
 };
+
+// 100 MHz constant-rate stamp, workgroup-comparable (diagnostics builds only)
+__device__ __forceinline__ unsigned long long realtime() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) :: "memory");
+  return t;
+}
 
 template <bool KC, int BK>
 struct Stage {
@@ -553,7 +562,7 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16r_kernel(PParams pp) {
 // Tile 256 x TN (TN = 256 or 128), 8 waves 2 (M) x 4 (N), each 128 x TN/4 = 4 x NI 32x32
 // accumulators. TN = 128 doubles the tile count of a narrow GEMM (N ~ 500: the hidden encoder
 // and decoder layers) so it fills the chip without split-K slabs and their reduction.
-template <bool AT, bool BT, int EPI, bool TE, int TN>
+template <bool AT, bool BT, int EPI, bool TE, int TN, bool ST = false>
 __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   constexpr int BK = 64;
   constexpr int NI = TN / 128;
@@ -563,6 +572,12 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   constexpr int NF = NI + 4;                   // fragments per wave per k16-step (B first)
   const Params& p = pp.g;
   if (epi_skip<EPI>(p.epi)) return;
+  unsigned long long st0 = 0, st1 = 0, st2 = 0;
+  if constexpr (ST) {
+    __builtin_amdgcn_sched_barrier(0);
+    st0 = realtime();
+    __builtin_amdgcn_sched_barrier(0);
+  }
   __shared__ __attribute__((aligned(16))) short smem[3 * IMA + 2 * IMB];  // A slots | B slots
 
   const int tid = threadIdx.x;
@@ -655,6 +670,11 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
     }
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    if constexpr (ST) {
+      __builtin_amdgcn_sched_barrier(0);
+      st1 = realtime();
+      __builtin_amdgcn_sched_barrier(0);
+    }
     next_b();
     sb_q[0] = 0; sb_q[1] = bsl;
     pend_a = next_a();
@@ -724,13 +744,33 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (ST) {
+    __builtin_amdgcn_sched_barrier(0);
+    st2 = realtime();
+    __builtin_amdgcn_sched_barrier(0);
+  }
   if constexpr (TE) epilogue_rm<EPI, 4, NI, 4, WNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag);
   else epilogue_g<EPI, 4, NI, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
+  if constexpr (ST) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const unsigned long long st3 = realtime();
+    if (threadIdx.x == 0) {
+      unsigned long long* o = pp.stamps + 4 * (size_t)blockIdx.x;
+      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3;
+    }
+  }
 }
 
 template <bool AT, bool BT, int EPI, bool TE, int TN>
 hipError_t launch_q(const PParams& p, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
+  if constexpr (EPI == EPI_ACT && TE && !AT && !BT) {  // stamped diagnostics build (bench only)
+    if (p.stamps) {
+      hipLaunchKernelGGL((gemm_bf16q_kernel<AT, BT, EPI, TE, TN, true>), dim3(nwg), dim3(WNT), 0, st, p);
+      return hipGetLastError();
+    }
+  }
   hipLaunchKernelGGL((gemm_bf16q_kernel<AT, BT, EPI, TE, TN>), dim3(nwg), dim3(WNT), 0, st, p);
   return hipGetLastError();
 }
@@ -762,13 +802,20 @@ hipError_t launch_q_t(const PParams& p, bool at, bool bt, hipStream_t st) {
 // the stage iteration it-1 read, and waited for (vmcnt(0)) at the top of it+1.
 constexpr int TT = 128, TNT = 256;
 
-template <bool AT, bool BT, int EPI, bool TE>
+// BK x DEPTH: 64 x 2 stages (one k-tile in flight, vmcnt(0) at each barrier) or 32 x 4 (three
+// in flight behind a counted vmcnt and a raw barrier), both 64 KB of LDS.
+template <bool AT, bool BT, int EPI, bool TE, bool ST = false, int BK = 64, int DEPTH = 2>
 __global__ __launch_bounds__(TNT, 2) void gemm_bf16t_kernel(PParams pp) {
-  constexpr int BK = 64;
   constexpr int IMG = TT * BK;  // bf16 elements per operand image
   const Params& p = pp.g;
   if (epi_skip<EPI>(p.epi)) return;
-  __shared__ __attribute__((aligned(16))) short smem[2 * 2 * IMG];  // [stage][A | B] = 64 KB
+  unsigned long long st0 = 0, st1 = 0, st2 = 0;
+  if constexpr (ST) {
+    __builtin_amdgcn_sched_barrier(0);
+    st0 = realtime();
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  __shared__ __attribute__((aligned(16))) short smem[DEPTH * 2 * IMG];  // [stage][A | B] = 64 KB
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -803,14 +850,29 @@ __global__ __launch_bounds__(TNT, 2) void gemm_bf16t_kernel(PParams pp) {
     if (++ikt == nkt) { ikt = 0; ++ipr; }
   };
   constexpr int NRD = 2 * WLoad<!AT, BK, TT, 4>::NRD + 2 * WLoad<BT, BK, TT, 4>::NRD;
+  constexpr int G = WLoad<!AT, BK, TT, 4>::NG + WLoad<BT, BK, TT, 4>::NG;  // DMA instrs per tile
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
-  if (total > 0) issue(0);
+#pragma unroll
+  for (int s = 0; s < DEPTH - 1; ++s)
+    if (s < total) issue(s);
   for (int it = 0; it < total; ++it) {
-    const int stage = it & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int stage = it % DEPTH;
+    if constexpr (DEPTH == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      const int issued = min(total, it + DEPTH - 1);
+      wait_dma<G>(issued - it - 1);  // this wave's copies of tile it have landed
+    }
     __builtin_amdgcn_s_barrier();  // tile it landed for every wave; stage it-1 no longer read
     asm volatile("" ::: "memory");
-    if (it + 1 < total && !(pp.diag & 1)) issue(stage ^ 1);
+    if constexpr (ST) {
+      if (it == 0) {
+        __builtin_amdgcn_sched_barrier(0);
+        st1 = realtime();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+    if (it + DEPTH - 1 < total && !(pp.diag & 1)) issue((it + DEPTH - 1) % DEPTH);
     const short* sa = smem + stage * 2 * IMG;
     const short* sb = sa + IMG;
     const unsigned la0 = lds0 + 2u * (unsigned)(stage * 2 * IMG);
@@ -843,14 +905,50 @@ __global__ __launch_bounds__(TNT, 2) void gemm_bf16t_kernel(PParams pp) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if constexpr (ST) {
+    __builtin_amdgcn_sched_barrier(0);
+    st2 = realtime();
+    __builtin_amdgcn_sched_barrier(0);
+  }
   if constexpr (TE) epilogue_rm<EPI, 2, 2, 2, TNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag);
   else epilogue_g<EPI, 2, 2, TT, 2>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
+  if constexpr (ST) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const unsigned long long st3 = realtime();
+    if (threadIdx.x == 0) {
+      unsigned long long* o = pp.stamps + 4 * (size_t)blockIdx.x;
+      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3;
+    }
+  }
+}
+
+// MVAE_TWIN_BK (diagnostics A/B): 32 = the 4-stage BK-32 pipeline, else 64 x 2 stages
+static int twin_bk() {
+  static const int bk = [] {
+    const char* v = std::getenv("MVAE_TWIN_BK");
+    return v && std::atoi(v) == 32 ? 32 : 64;
+  }();
+  return bk;
 }
 
 template <bool AT, bool BT, int EPI, bool TE>
 hipError_t launch_tw(const PParams& p, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
-  hipLaunchKernelGGL((gemm_bf16t_kernel<AT, BT, EPI, TE>), dim3(nwg), dim3(TNT), 0, st, p);
+  const bool deep = twin_bk() == 32;
+  if constexpr (EPI == EPI_ACT && TE) {  // the stamped diagnostics build (mvae_bench_gemm only)
+    if (p.stamps) {
+      if (deep)
+        hipLaunchKernelGGL((gemm_bf16t_kernel<AT, BT, EPI, TE, true, 32, 4>), dim3(nwg), dim3(TNT), 0, st, p);
+      else
+        hipLaunchKernelGGL((gemm_bf16t_kernel<AT, BT, EPI, TE, true>), dim3(nwg), dim3(TNT), 0, st, p);
+      return hipGetLastError();
+    }
+  }
+  if (deep)
+    hipLaunchKernelGGL((gemm_bf16t_kernel<AT, BT, EPI, TE, false, 32, 4>), dim3(nwg), dim3(TNT), 0, st, p);
+  else
+    hipLaunchKernelGGL((gemm_bf16t_kernel<AT, BT, EPI, TE>), dim3(nwg), dim3(TNT), 0, st, p);
   return hipGetLastError();
 }
 
@@ -1042,6 +1140,7 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   p.B = d.Bp; p.pB = d.pB;
   p.dyn = d.dynA;
   p.diag = d.diag;
+  p.stamps = d.stamps;
   // plane pairs (i, j), i + j < max(nA, nB); the pairs with i = 0 first
   int n = 0;
   const int T = d.nA > d.nB ? d.nA : d.nB;

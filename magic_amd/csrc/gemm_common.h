@@ -28,18 +28,40 @@ constexpr int TN_TWIN = 1;  // Params::tn of the 128 x 128 twin kernel (gemm_bf1
 // tanh from the hardware exp / reciprocal (v_exp_f32, v_rcp_f32) and an odd polynomial where
 // 1 - 2/(e^2x + 1) cancels: relative error < 2e-6 everywhere (the accurate tanhf costs ~50 VALU
 // instructions per element, which the hidden-layer epilogues could not hide)
+// (branch-free: both forms are evaluated and one selected, so an unrolled epilogue stays one
+// straight instruction stream)
 __device__ __forceinline__ float tanh_fast(float x) {
   const float ax = fabsf(x);
-  if (ax < 0.125f) {  // Taylor to x^7; the x^9 term is < 3e-10 |x| here
-    const float x2 = x * x;
-    return x * (1.f + x2 * (-0.333333333f + x2 * (0.133333333f + x2 * -0.0539682540f)));
-  }
-  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(__expf(2.f * ax) + 1.f);
-  return copysignf(t, x);
+  const float x2 = x * x;  // |x| < 1/8: Taylor to x^7; the x^9 term is < 3e-10 |x| there
+  const float p = x * (1.f + x2 * (-0.333333333f + x2 * (0.133333333f + x2 * -0.0539682540f)));
+  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(ax * 2.8853900817779268f) + 1.f);
+  return ax < 0.125f ? p : copysignf(t, x);
 }
+__device__ __forceinline__ float elu_fast(float v) { return v < 0.f ? __expf(v) - 1.f : v; }
 __device__ __forceinline__ float act_f(float v, int act) {
   if (act == ACT_TANH) return tanh_fast(v);
-  return v < 0.f ? __expf(v) - 1.f : v;  // TF elu: exp(x) - 1 for x < 0
+  return elu_fast(v);  // TF elu: exp(x) - 1 for x < 0
+}
+// the activation (derivative) of n values, the act switch hoisted out of the element loop
+template <int n>
+__device__ __forceinline__ void act_n(float (&v)[n], int act) {
+  if (act == ACT_TANH) {
+#pragma unroll
+    for (int j = 0; j < n; ++j) v[j] = tanh_fast(v[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < n; ++j) v[j] = elu_fast(v[j]);
+  }
+}
+template <int n>
+__device__ __forceinline__ void dact_n(float (&v)[n], const float (&y)[n], int act) {
+  if (act == ACT_TANH) {
+#pragma unroll
+    for (int j = 0; j < n; ++j) v[j] = v[j] * (1.f - y[j] * y[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < n; ++j) v[j] = y[j] < 0.f ? v[j] * (y[j] + 1.f) : v[j];
+  }
 }
 __device__ __forceinline__ float dact_f(float g, float y, int act) {
   if (act == ACT_TANH) return g * (1.f - y * y);  // TF TanhGrad
@@ -162,6 +184,25 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
         }
       }
     }
+    // ACT / DACT: the activation over the block's 16 x NI values with the act switch hoisted
+    // out of the element loop (per-element runtime selects broke the epilogue into branches)
+    float av[16 * NI];
+    if constexpr (EPI == EPI_ACT || EPI == EPI_DACT) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) av[r * NI + ni] = acc[mi][ni][r];
+      if constexpr (EPI == EPI_ACT) {
+        act_n(av, e.act);
+      } else {
+        float yv[16 * NI];
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) yv[r * NI + ni] = sv[r][ni];
+        dact_n(av, yv, e.act);
+      }
+    }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int row = rbase + mi * 32 + (r & 3) + 8 * (r >> 2);
@@ -172,6 +213,7 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
         if (row < p.M && col < p.N) {
           const size_t o = (size_t)row * p.ldc + col;
           float v = acc[mi][ni][r];
+          if constexpr (EPI == EPI_ACT || EPI == EPI_DACT) v = av[r * NI + ni];
           if constexpr (BCE) {
             const float yv = sigmoid_fast(v);
             const float xv = sv[r][ni];
@@ -180,9 +222,7 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
             v = (yv - xv) * e.scale;
             if (e.y) e.y[(size_t)row * e.ldy + col] = yv;
           }
-          if constexpr (EPI == EPI_ACT) v = act_f(v, e.act);
           if constexpr (EPI == EPI_SIGMOID) v = sigmoid_f(v);
-          if constexpr (EPI == EPI_DACT) v = dact_f(v, sv[r][ni], e.act);
           if (e.c32) C[o] = v;
           if (cp) store_planes(cp, e.pc, e.ncp, o, v);
         }
@@ -351,19 +391,23 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
           }
         }
         float yv[8];
+        if constexpr (BCE) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          if constexpr (BCE) {
+          for (int j = 0; j < 8; ++j) {
             if (diag & 8) { yv[j] = v[j]; rs += v[j] * sv[j]; v[j] = (yv[j] - sv[j]) * e.scale; continue; }
             yv[j] = sigmoid_fast(v[j]);
             // -log(y^x (1-y)^(1-x)) with TF pow(0,0) = 1 (no epsilon), 11a/vae.py:266-269
             if (j < nv) rs += bce_term(yv[j], sv[j]);
             v[j] = (yv[j] - sv[j]) * e.scale;
           }
-          if constexpr (EPI == EPI_ACT) v[j] = act_f(v[j], e.act);
-          if constexpr (EPI == EPI_SIGMOID) v[j] = sigmoid_f(v[j]);
-          if constexpr (EPI == EPI_DACT) v[j] = dact_f(v[j], sv[j], e.act);
         }
+        if constexpr (EPI == EPI_ACT)
+          if (!(diag & 8)) act_n(v, e.act);
+        if constexpr (EPI == EPI_SIGMOID) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) v[j] = sigmoid_f(v[j]);
+        }
+        if constexpr (EPI == EPI_DACT) dact_n(v, sv, e.act);
         const size_t o = (size_t)row * p.ldc + col0;
         if (diag & 2) {
         } else if (full) {

@@ -263,13 +263,10 @@ __global__ void splitk_reduce4_kernel(const float* __restrict__ ws, int split, i
     if constexpr (EPI == EPI_DACT) {
       const int ar = row >= e.remap_split ? row - e.remap_shift : row;
       const size_t ai = (size_t)ar * e.ld_aux + col;
-      if (e.auxp) {
+      float y[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = dact_f(v[j], bf16_bits_to_f32(e.auxp[ai + j]), e.act);
-      } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = dact_f(v[j], e.aux[ai + j], e.act);
-      }
+      for (int j = 0; j < 4; ++j) y[j] = e.auxp ? bf16_bits_to_f32(e.auxp[ai + j]) : e.aux[ai + j];
+      dact_n(v, y, e.act);
     }
     const size_t o = (size_t)row * ldc + col;
     if (e.c32) *reinterpret_cast<float4*>(c + o) = make_float4(v[0], v[1], v[2], v[3]);

@@ -75,6 +75,13 @@ struct mvae_ctx {
   float *dzd2 = nullptr, *dzd1 = nullptr, *dzdec = nullptr, *dhead = nullptr;
   std::vector<float*> dzl;  // dZ of every encoder layer [4B][lddz] (all live until its wgrad)
   int enc_part1 = 0;        // bwd_enc[0, enc_part1): dgrad chain + layer-0 wgrad
+  // the layer-0 weight gradient in R row chunks (option "wgrad0_chunks", R = 2, 4, 8): chunk r
+  // covers rows [w0m[R][r], w0m[R][r+1]) of the [W_0; b_0] block, one backward part each, so a
+  // data-parallel host all-reduces each chunk while the next one computes (R = 1: one GEMM)
+  int w0_chunks = 1;
+  std::vector<GemmDesc> w0c[9];
+  std::vector<int> w0m[9];
+  int bpart = 0;            // next backward part expected (phase 4)
   float* zgen = nullptr;
   int dhead32 = 1;           // latent_bwd writes fp32 dhead rows (some fp32 GEMM reads them)
   float* ws = nullptr;       // split-K slabs of GEMMs on the caller's stream
@@ -535,12 +542,14 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   }
   build_schedule(c);
   if (const char* nv = std::getenv("MVAE_NO_VALU"); nv && *nv == '1') c->valu = false;
-  // kernel A/B switch (diagnostics): MVAE_TWIN=0 plans the bf16 DMA GEMMs on the ring kernels
-  // only (round-2 plan), 2 forces the 128x128 twin kernel wherever a ring kernel would run
-  int twin_mode = 1;
+  // kernel A/B switch (diagnostics): the bf16 DMA GEMMs are planned on the ring kernels only
+  // (default, MVAE_TWIN=0: the 128x128 twin kernel measured slower on every step shape, e.g. C3
+  // 2.263 vs 2.331 ms/step with the planner's twin choices, profiles/r3/README.md); MVAE_TWIN=1
+  // lets the planner choose it, 2 forces it wherever a ring kernel would run
+  int twin_mode = 0;
+  if (const char* tw = std::getenv("MVAE_TWIN"); tw && (*tw == '1' || *tw == '2')) twin_mode = *tw - '0';
   bool dact_planes = true;  // MVAE_DACT_F32AUX=1: bf16-mode DACT reads the fp32 activations (A/B)
   if (const char* fa = std::getenv("MVAE_DACT_F32AUX"); fa && *fa == '1') dact_planes = false;
-  if (const char* tw = std::getenv("MVAE_TWIN"); tw && (*tw == '0' || *tw == '2')) twin_mode = *tw - '0';
   const int gp = cfg->precision == MVAE_PREC_BF16 ? GEMM_BF16
                  : (cfg->precision == MVAE_PREC_F32X ? GEMM_F32X : GEMM_F32);
   c->np = gp == GEMM_BF16 ? 1 : (gp == GEMM_F32X ? 3 : 0);
@@ -673,8 +682,27 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
         mvae_destroy(c);
         return MVAE_EINVAL;
       }
+  {  // layer-0 weight-gradient row chunks (see w0c): the wired GEMM re-pointed at row ranges
+    const GemmDesc& w = c->bwd_enc[c->nenc];
+    for (int R : {2, 4, 8}) {
+      const int per = ((w.M + R - 1) / R + 255) / 256 * 256;
+      for (int m0 = 0; m0 < w.M; m0 += per) {
+        GemmDesc d = w;
+        const int m1 = std::min(w.M, m0 + per);
+        d.M = m1 - m0;
+        d.A = w.A + m0;                  // A stored [K][M] (at): the chunk's columns
+        if (d.Ap) d.Ap = w.Ap + m0;
+        d.C = w.C + (size_t)m0 * w.ldc;  // output rows
+        c->w0c[R].push_back(d);
+        c->w0m[R].push_back(m0);
+      }
+      c->w0m[R].push_back(w.M);
+    }
+  }
   size_t ws = 0;
   auto wsz = [&](const GemmDesc& d) { ws = std::max(ws, gemm_workspace_elems(d)); };
+  for (int R : {2, 4, 8})
+    for (auto& d : c->w0c[R]) wsz(d);
   for (auto& d : c->fwd_enc) wsz(d);
   for (auto& d : c->bwd_dec) wsz(d);
   for (auto& d : c->bwd_enc) wsz(d);
@@ -989,17 +1017,26 @@ extern "C" int mvae_metric(mvae_ctx* ctx, const float* areas, void* stream) {
   return MVAE_OK;
 }
 
-// Backward in three parts (phase 2 -> 4 -> 5 -> 3); after part k the ranges
-// mvae_grad_range(ctx, k, i, ...) hold final (rank-local) gradients on the caller's stream.
+// Backward in R + 2 parts (R = the layer-0 weight-gradient chunks, option "wgrad0_chunks";
+// phase 2 -> 4 ... -> 3); after part k the ranges mvae_grad_range(ctx, k, i, ...) hold final
+// (rank-local) gradients on the caller's stream. Part 0: the decoder; part 1: the latent head
+// backward, the encoder dgrad chain and layer-0 chunk 0; parts 2 .. R: layer-0 chunks 1 .. R-1
+// (the conv tower's backward after the last chunk); part R + 1: joins the side stream.
 // The dgrad chain (decoder output -> ... -> encoder layer 1) runs on the caller's stream; each
 // weight gradient runs on the side stream as soon as its dZ exists, beside the chain (the
 // chain's GEMMs leave CUs idle: few tiles, split-K reductions). Part 0 joins the decoder's
-// weight gradients, part 2 the encoder's (part 1 ends with the layer-0 weight gradient on the
+// weight gradients, the last part the encoder's (the layer-0 weight gradient runs on the
 // caller's stream). join_dec = false (the single-call mvae_backward) leaves the decoder's
 // weight gradients running beside the encoder chain too.
+// layer-0 weight-gradient chunks in use: the option's R, or fewer when the block has fewer rows
+// than R chunks of 256 (chunk boundaries are tile multiples)
+static int w0n(const mvae_ctx* c) { return c->w0_chunks == 1 ? 1 : (int)c->w0c[c->w0_chunks].size(); }
+static int nparts(const mvae_ctx* c) { return w0n(c) + 2; }
+
 static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec) {
   auto c = ctx;
   int rc;
+  const int R = w0n(c);
   const bool two = c->use_side && c->side;
   hipStream_t sd = two ? c->side : st;
   auto fork = [&]() -> int { return two ? stream_wait(c, st, sd) : MVAE_OK; };
@@ -1009,6 +1046,36 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
     if (!c->side || !c->side_pending) return MVAE_OK;
     c->side_pending = false;
     return stream_wait(c, c->side, st);
+  };
+  const int n = c->nenc;
+  auto w0chunk = [&](int r) -> int {  // layer-0 weight gradient, chunk r of R
+    const GemmDesc& d = R == 1 ? c->bwd_enc[n] : c->w0c[c->w0_chunks][r];
+    return run(c, d, st, c->bwd_enc_r[n]);
+  };
+  auto tower = [&]() -> int {  // back through the conv tower (its gradients final after it)
+    if (!c->conv) return MVAE_OK;
+    const ConvTower& T = c->tower;
+    float* g1 = c->grads;
+    float* g2 = c->grads + c->n_all;
+    int rc2;
+    if ((rc2 = run(c, c->bwd_feat, st, c->bwd_feat_r))) return rc2;
+    {
+      TIMED("pool2_bwd");
+      MV_CHECK(launch_pool2_bwd(T, c->dxf, c->ldf, c->B, st));
+    }
+    {
+      TIMED("conv2_wgrad");
+      MV_CHECK(launch_conv2_wgrad(T, c->B, g1 + c->cv2.off, g2 + c->cv2.off, st));
+    }
+    {
+      TIMED("conv2_dgrad");
+      MV_CHECK(launch_conv2(T, false, T.da2, T.da2b, c->theta + c->cv2.off, T.w2d, T.dn1, 4 * c->B, st));
+    }
+    {
+      TIMED("conv1_wgrad");
+      MV_CHECK(launch_conv1_wgrad(T, c->xs, c->ldx, c->B, g1 + c->cv1.off, g2 + c->cv1.off, st));
+    }
+    return MVAE_OK;
   };
   if (part == 0) {
     // bwd_dec: W_out, D_out, W_d2, D_d2, W_d1, D_z
@@ -1023,7 +1090,6 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
     if ((rc = run(c, c->bwd_dec[4], sd, c->bwd_dec_r[4]))) return rc;
     if ((rc = run(c, c->bwd_dec[5], st, c->bwd_dec_r[5]))) return rc;
     if (join_dec && (rc = join())) return rc;
-    ctx->phase = 4;
   } else if (part == 1) {
     {
       TIMED("latent_bwd");
@@ -1034,7 +1100,6 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
     }
     // bwd_enc: [dgrad(n) .. dgrad(1), wgrad(0) | wgrad(n), wgrad(n-1) .. wgrad(1)]; dgrad(i)
     // produces dZ_{i-1}, wgrad(i) needs dZ_i (dgrad(n) = the head's: dZ of layer n-1)
-    const int n = c->nenc;
     auto wg = [&](int i) -> const GemmDesc& { return c->bwd_enc[c->enc_part1 + (n - i)]; };
     auto wr = [&](int i) { return c->bwd_enc_r[c->enc_part1 + (n - i)]; };
     if ((rc = fork())) return rc;
@@ -1048,42 +1113,27 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
         if ((rc = run(c, wg(i - 1), sd, wr(i - 1)))) return rc;
       }
     }
-    if ((rc = run(c, c->bwd_enc[n], st, c->bwd_enc_r[n]))) return rc;  // wgrad(0)
-    if (c->conv) {  // back through the tower (its gradients are final at the end of part 1)
-      const ConvTower& T = c->tower;
-      float* g1 = c->grads;
-      float* g2 = c->grads + c->n_all;
-      if ((rc = run(c, c->bwd_feat, st, c->bwd_feat_r))) return rc;
-      {
-        TIMED("pool2_bwd");
-        MV_CHECK(launch_pool2_bwd(T, c->dxf, c->ldf, c->B, st));
-      }
-      {
-        TIMED("conv2_wgrad");
-        MV_CHECK(launch_conv2_wgrad(T, c->B, g1 + c->cv2.off, g2 + c->cv2.off, st));
-      }
-      {
-        TIMED("conv2_dgrad");
-        MV_CHECK(launch_conv2(T, false, T.da2, T.da2b, c->theta + c->cv2.off, T.w2d, T.dn1, 4 * c->B, st));
-      }
-      {
-        TIMED("conv1_wgrad");
-        MV_CHECK(launch_conv1_wgrad(T, c->xs, c->ldx, c->B, g1 + c->cv1.off, g2 + c->cv1.off, st));
-      }
-    }
-    ctx->phase = 5;
+    if ((rc = w0chunk(0))) return rc;
+    if (R == 1 && (rc = tower())) return rc;
+  } else if (part <= R) {
+    if ((rc = w0chunk(part - 1))) return rc;
+    if (part == R && (rc = tower())) return rc;
   } else {
     if ((rc = join())) return rc;
-    ctx->phase = 3;
   }
+  c->bpart = part + 1;
+  ctx->phase = part == R + 1 ? 3 : 4;
   return MVAE_OK;
 }
 
+extern "C" int mvae_backward_nparts(mvae_ctx* ctx) { return ctx ? nparts(ctx) : MVAE_EINVAL; }
+
 extern "C" int mvae_backward_part(mvae_ctx* ctx, int part, void* stream) {
   if (!ctx) return MVAE_EINVAL;
-  const int need = part == 0 ? 2 : (part == 1 ? 4 : 5);
-  if (part < 0 || part > 2) return fail(ctx, MVAE_EINVAL, "backward part must be 0, 1 or 2");
-  if (ctx->phase != need) return fail(ctx, MVAE_ESTATE, "mvae_backward_part out of order");
+  if (part < 0 || part >= nparts(ctx))
+    return fail(ctx, MVAE_EINVAL, "backward part must be in [0, mvae_backward_nparts)");
+  const bool ok = part == 0 ? ctx->phase == 2 : (ctx->phase == 4 && ctx->bpart == part);
+  if (!ok) return fail(ctx, MVAE_ESTATE, "mvae_backward_part out of order");
   return backward_part(ctx, part, (hipStream_t)stream, true);
 }
 
@@ -1091,7 +1141,7 @@ extern "C" int mvae_backward(mvae_ctx* ctx, void* stream) {
   if (!ctx) return MVAE_EINVAL;
   if (ctx->phase != 2) return fail(ctx, MVAE_ESTATE, "mvae_backward before mvae_metric");
   int rc;
-  for (int part = 0; part < 3; ++part)
+  for (int part = 0; part < nparts(ctx); ++part)
     if ((rc = backward_part(ctx, part, (hipStream_t)stream, false))) return rc;
   return MVAE_OK;
 }
@@ -1106,20 +1156,45 @@ extern "C" int mvae_set_option(mvae_ctx* ctx, const char* name, int value) {
     ctx->use_side = value != 0;
     return MVAE_OK;
   }
+  if (k == "wgrad0_chunks") {
+    if (value != 1 && value != 2 && value != 4 && value != 8)
+      return fail(ctx, MVAE_EINVAL, "wgrad0_chunks must be 1, 2, 4 or 8");
+    if (ctx->phase == 4) return fail(ctx, MVAE_ESTATE, "wgrad0_chunks cannot change mid-backward");
+    ctx->w0_chunks = value;
+    return MVAE_OK;
+  }
   return fail(ctx, MVAE_EINVAL, "unknown option " + k);
 }
 
+// The ranges of grads [g1 (n_all) | g2 (n_enc)] that part `part` finishes: part 0 the decoder
+// slice of g1; parts 1 .. R the layer-0 rows of chunk part-1 in g1 and in g2 (the last chunk up
+// to the end of the layer-0 block, plus the conv-tower blocks in front of it); part R + 1 the
+// rest of the encoder slice in g1 and g2. Together they cover grads exactly once.
 extern "C" int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* count) {
   if (!ctx || !ptr || !count) return MVAE_EINVAL;
+  const int R = w0n(ctx);
+  const Block& b0 = ctx->enc[0];
   const size_t l1 = ctx->nenc > 1 ? ctx->enc[1].off : ctx->head.off;  // end of the layer-0 block
   float* g1 = ctx->grads;
   float* g2 = ctx->grads + ctx->n_all;
-  if (part == 0 && index == 0) { *ptr = g1 + ctx->n_enc; *count = ctx->n_all - ctx->n_enc; return MVAE_OK; }
-  if (part == 1 && index == 0) { *ptr = g1; *count = l1; return MVAE_OK; }
-  if (part == 1 && index == 1) { *ptr = g2; *count = l1; return MVAE_OK; }
-  if (part == 2 && index == 0) { *ptr = g1 + l1; *count = ctx->n_enc - l1; return MVAE_OK; }
-  if (part == 2 && index == 1) { *ptr = g2 + l1; *count = ctx->n_enc - l1; return MVAE_OK; }
-  return MVAE_EINVAL;
+  std::vector<std::pair<float*, size_t>> r;
+  if (part == 0) {
+    r.push_back({g1 + ctx->n_enc, ctx->n_all - ctx->n_enc});
+  } else if (part >= 1 && part <= R) {
+    const int m0 = R == 1 ? 0 : ctx->w0m[ctx->w0_chunks][part - 1];
+    const int m1 = R == 1 ? b0.K + 1 : ctx->w0m[ctx->w0_chunks][part];
+    const size_t a = b0.off + (size_t)m0 * b0.ld;
+    const size_t e = part == R ? l1 : b0.off + (size_t)m1 * b0.ld;
+    for (float* g : {g1, g2}) r.push_back({g + a, e - a});
+    if (part == R && b0.off > 0)  // conv-tower blocks / leading alignment
+      for (float* g : {g1, g2}) r.push_back({g, b0.off});
+  } else if (part == R + 1) {
+    for (float* g : {g1, g2}) r.push_back({g + l1, ctx->n_enc - l1});
+  }
+  if (index < 0 || index >= (int)r.size()) return MVAE_EINVAL;
+  *ptr = r[index].first;
+  *count = r[index].second;
+  return MVAE_OK;
 }
 
 extern "C" int mvae_adam(mvae_ctx* ctx, void* stream) {
@@ -1440,6 +1515,46 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   float ms = 0.f;
   if (e == hipSuccess) e = hipEventElapsedTime(&ms, t0, t1);
   *avg_ms = ms / iters;
+  // MVAE_STAMPS=1 (diagnostics): one more launch of the stamped twin-kernel build (ACT epilogue),
+  // per-workgroup segment times (us, 100 MHz stamps) summarised on stderr
+  if (const char* sp = std::getenv("MVAE_STAMPS"); e == hipSuccess && sp && *sp == '1') {
+    const int nmax = 1 << 20;
+    unsigned long long* sb = nullptr;
+    e = hipMalloc(&sb, (size_t)4 * nmax * 8);
+    if (e == hipSuccess) e = hipMemsetAsync(sb, 0, (size_t)4 * nmax * 8, st);
+    GemmDesc ds = d;
+    ds.stamps = sb;
+    if (e == hipSuccess) e = gemm_run(ds, ws, ws_n, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    std::vector<unsigned long long> h((size_t)4 * nmax);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), sb, h.size() * 8, hipMemcpyDeviceToHost);
+    if (sb) (void)hipFree(sb);
+    int n = 0;
+    unsigned long long lo = ~0ull, hi = 0;
+    double seg[3] = {0, 0, 0};
+    for (int i = 0; i < nmax && e == hipSuccess; ++i) {
+      const unsigned long long* q = &h[4 * (size_t)i];
+      if (!q[0]) continue;
+      ++n;
+      lo = std::min(lo, q[0]); hi = std::max(hi, q[3]);
+      for (int k = 0; k < 3; ++k) seg[k] += (double)(q[k + 1] - q[k]) * 0.01;
+    }
+    if (n) {
+      std::vector<double> st0s, ends;
+      for (int i = 0; i < nmax; ++i) {
+        const unsigned long long* q = &h[4 * (size_t)i];
+        if (!q[0]) continue;
+        st0s.push_back((q[0] - lo) * 0.01);
+        ends.push_back((q[3] - lo) * 0.01);
+      }
+      std::sort(st0s.begin(), st0s.end());
+      std::sort(ends.begin(), ends.end());
+      std::fprintf(stderr, "[stamps] M %d N %d K %d: %d workgroups, span %.2f us; mean per WG: prologue %.2f, "
+                   "k-loop %.2f, epilogue %.2f us; start p50/p90/max %.2f/%.2f/%.2f; end p10/p50/max %.2f/%.2f/%.2f\n",
+                   M, N, K, n, (hi - lo) * 0.01, seg[0] / n, seg[1] / n, seg[2] / n,
+                   st0s[n / 2], st0s[n * 9 / 10], st0s[n - 1], ends[n / 10], ends[n / 2], ends[n - 1]);
+    }
+  }
   if (t0) (void)hipEventDestroy(t0);
   if (t1) (void)hipEventDestroy(t1);
   for (float* p : {A, Bm, Cm, ws, aux, rowpart}) if (p) (void)hipFree(p);

@@ -152,7 +152,9 @@ __device__ __forceinline__ void philox(uint32_t c[4], uint32_t k0, uint32_t k1) 
 // The 4 normals of Philox block q of call `counter`: global elements 4q .. 4q+3 of the stream
 // (Box-Muller on the block's two 32-bit pairs). The sampler kernel and the fused latent kernels
 // (which regenerate eps in registers instead of reading it) share this code, so a regenerated
-// value is bit-identical to the sampled one.
+// value is bit-identical to the sampled one. Hardware transcendentals (v_log_f32 = log2,
+// v_sin/cos_f32 of 2*pi*x, v_sqrt_f32; ~1 ulp): the latent kernels regenerate 3*B*L normals in
+// the forward and again in the backward, and the accurate libm forms made them VALU-bound.
 __device__ __forceinline__ void normal4(uint64_t q, uint64_t seed, uint64_t counter, float (&r)[4]) {
   uint32_t c[4] = {(uint32_t)q, (uint32_t)(q >> 32), (uint32_t)counter, (uint32_t)(counter >> 32)};
   philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
@@ -161,11 +163,10 @@ __device__ __forceinline__ void normal4(uint64_t q, uint64_t seed, uint64_t coun
   for (int j = 0; j < 2; ++j) {
     const float u1 = __fmul_rn(__fadd_rn((float)c[2 * j], 0.5f), inv);  // (0,1)
     const float u2 = __fmul_rn(__fadd_rn((float)c[2 * j + 1], 0.5f), inv);
-    const float rad = sqrtf(__fmul_rn(-2.f, logf(u1)));
-    float sn, co;
-    sincosf(__fmul_rn(6.283185307179586f, u2), &sn, &co);
-    r[2 * j] = __fmul_rn(rad, co);
-    r[2 * j + 1] = __fmul_rn(rad, sn);
+    // -2 ln u1 = -2 ln2 log2 u1
+    const float rad = __builtin_amdgcn_sqrtf(__fmul_rn(-1.3862943611198906f, __builtin_amdgcn_logf(u1)));
+    r[2 * j] = __fmul_rn(rad, __builtin_amdgcn_cosf(u2));      // cos(2 pi u2)
+    r[2 * j + 1] = __fmul_rn(rad, __builtin_amdgcn_sinf(u2));  // sin(2 pi u2)
   }
 }
 
@@ -225,10 +226,14 @@ __device__ __forceinline__ void eps_get(const EpsSrc& es, int blk, int b, int i,
   }
 }
 
-// z = mu + sqrt(exp(s)) * eps (11a/vae.py:371-377), one explicit rounding sequence shared by
-// the forward and the backward (which recomputes z instead of reading it)
+// sigma = sqrt(exp(s)) = exp2(s log2(e) / 2) on v_exp_f32, and z = mu + sigma * eps
+// (11a/vae.py:371-377): one explicit rounding sequence shared by the forward and the backward
+// (which recomputes z instead of reading it)
+__device__ __forceinline__ float sigma_of(float s) {
+  return __builtin_amdgcn_exp2f(__fmul_rn(s, 0.72134752044448170f));
+}
 __device__ __forceinline__ float reparam(float mu, float s, float e) {
-  return __fadd_rn(mu, __fmul_rn(sqrtf(expf(s)), e));
+  return __fadd_rn(mu, __fmul_rn(sigma_of(s), e));
 }
 
 __device__ __forceinline__ void ld4(const float* p, float (&v)[4]) {
@@ -288,7 +293,7 @@ __global__ void latent_fwd_kernel(const float* __restrict__ ms, EpsSrc es, float
     }
 #pragma unroll
     for (int j = 0; j < W; ++j) {
-      kl += 1.f + sl[j] - mul[j] * mul[j] - expf(sl[j]);
+      kl += 1.f + sl[j] - mul[j] * mul[j] - __expf(sl[j]);
       const float d = zz[1][j] - zz[0][j], q = zz[1][j] - zz[2][j];
       fd += d * d;
       sq += q * q;
@@ -499,8 +504,8 @@ __global__ void latent_bwd_kernel(const float* __restrict__ ms, EpsSrc es,
     const float zr = reparam(mu[0][j], sg[0][j], e[0][j]);
     const float zl = reparam(mu[1][j], sg[1][j], e[1][j]);
     const float zk = reparam(mu[2][j], sg[2][j], e[2][j]);
-    const float ex_l = expf(sg[1][j]);
-    const float sig_r = sqrtf(expf(sg[0][j])), sig_l = sqrtf(ex_l), sig_k = sqrtf(expf(sg[2][j]));
+    const float ex_l = __expf(sg[1][j]);
+    const float sig_r = sigma_of(sg[0][j]), sig_l = sigma_of(sg[1][j]), sig_k = sigma_of(sg[2][j]);
     const float def = 2.f * w * (zl - zr) * inv_bg;
     float dz2, dz3;  // g2 rows: lock, key
     if (metric == 1) {

@@ -193,7 +193,10 @@ class Engine:
     def backward(self):
         self._check(self.lib.mvae_backward(self.ctx, self.stream))
 
-    N_BACKWARD_PARTS = 3
+    @property
+    def N_BACKWARD_PARTS(self) -> int:
+        """Backward parts of the current schedule (2 + the layer-0 weight-gradient chunks)."""
+        return self.lib.mvae_backward_nparts(self.ctx)
 
     def backward_part(self, part: int):
         """Part ``part`` (0, 1, 2 in order) of ``backward``; see ``grad_ranges``."""

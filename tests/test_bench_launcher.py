@@ -33,5 +33,14 @@ def test_bench_self_launches_two_ranks_and_matches_one():
     # whole-job throughput: pairs of all ranks / max-over-ranks time
     assert abs(two["value"] - 16 * 3 / (two["ms_per_step"] * 3e-3)) <= 1e-3 * two["value"]
     for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "higher_is_better",
-              "vs_baseline", "dtype", "data", "roofline", "cpu_baseline"):
-        assert k in two
+              "vs_baseline", "dtype", "data", "roofline", "cpu_baseline", "h2d", "configs", "build_id"):
+        assert k in two and k in one
+    # the configs block: C3 / C5 on one GPU, C4 (C3's shape per rank) / C5 with N ranks, each
+    # with its own value and rooflines
+    assert set(one["configs"]) == {"C3", "C5"} and set(two["configs"]) == {"C4", "C5"}
+    for line in (one, two):
+        for cid, c in line["configs"].items():
+            for k in ("workload", "value", "ms_per_step", "global_batch", "per_gpu_batch", "roofline",
+                      "loss_roofline"):
+                assert k in c, (cid, k)
+    assert two["configs"]["C4"]["global_batch"] == 2 * two["configs"]["C4"]["per_gpu_batch"]

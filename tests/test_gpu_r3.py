@@ -113,3 +113,48 @@ def test_step_c2_f32x_twin_everywhere(monkeypatch):
     fp32 bar."""
     monkeypatch.setenv("MVAE_TWIN", "2")
     check_step(preset("8c", image_size=100, batch=4096, precision="f32x"), adam=False)
+
+
+# ------------------------------------------------------------------ chunked layer-0 gradient
+@pytest.mark.parametrize("chunks", [1, 2, 4, 8])
+@pytest.mark.parametrize("prec,conv", [("f32x", False), ("bf16", False), ("f32", True)])
+def test_wgrad0_chunks_tile_grads_and_match_backward(chunks, prec, conv):
+    """Option "wgrad0_chunks" = R: the backward in R + 2 parts; the ranges the parts report cover
+    MVAE_BUF_GRADS exactly once, and the chunked gradients equal the one-GEMM backward (the
+    chunk GEMMs plan their own split-K, so agreement is to the GEMM's rounding, not bitwise)."""
+    from magic_amd.engine import Engine
+    from tests.gpu_helpers import make_inputs, make_params, max_rel, to_dev
+    if conv:
+        cfg = preset("8c", image_size=20, batch=24, conv=True, precision=prec).replace(enc=(64, 40))
+    else:
+        cfg = preset("8c", image_size=40, batch=96, precision=prec).replace(enc=(300, 260))
+    eng = Engine(cfg, 0)
+    try:
+        P = make_params(cfg)
+        X, areas, eps = make_inputs(cfg, cfg.batch)
+        eng.load_params(P)
+        eng.forward(to_dev(X), to_dev(eps))
+        eng.metric(to_dev(areas))
+        eng.backward()
+        torch.cuda.synchronize()
+        ref = eng.grads.cpu().numpy().copy()
+        eng.set_option("wgrad0_chunks", chunks)
+        assert 3 <= eng.N_BACKWARD_PARTS <= chunks + 2  # fewer chunks than 256-row tiles allow
+        eng.load_params(P)
+        eng.forward(to_dev(X), to_dev(eps))
+        eng.metric(to_dev(areas))
+        cover = torch.zeros(eng.grads.numel(), dtype=torch.int32)
+        base = eng.grads.data_ptr()
+        for part in range(eng.N_BACKWARD_PARTS):
+            eng.backward_part(part)
+            for v in eng.grad_ranges(part):
+                off = (v.data_ptr() - base) // 4
+                cover[off:off + v.numel()] += 1
+        torch.cuda.synchronize()
+        assert int(cover.min()) == 1 and int(cover.max()) == 1, "ranges must tile grads exactly once"
+        got = eng.grads.cpu().numpy()
+        assert max_rel(got, ref) <= (1e-5 if prec != "bf16" else 1e-2), max_rel(got, ref)
+        with pytest.raises(Exception):
+            eng.set_option("wgrad0_chunks", 3)
+    finally:
+        eng.close()
