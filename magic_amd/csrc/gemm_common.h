@@ -28,14 +28,17 @@ constexpr int TN_TWIN = 1;  // Params::tn of the 128 x 128 twin kernel (gemm_bf1
 // tanh from the hardware exp / reciprocal (v_exp_f32, v_rcp_f32) and an odd polynomial where
 // 1 - 2/(e^2x + 1) cancels: relative error < 2e-6 everywhere (the accurate tanhf costs ~50 VALU
 // instructions per element, which the hidden-layer epilogues could not hide)
-// (branch-free: both forms are evaluated and one selected, so an unrolled epilogue stays one
-// straight instruction stream)
+// (branch-free: both forms are evaluated and one selected by v_cndmask -- the empty asm
+// statements pin both values, otherwise hipcc turns the select into a per-element exec-mask
+// branch around the exp / rcp, which made the epilogue several times slower)
 __device__ __forceinline__ float tanh_fast(float x) {
   const float ax = fabsf(x);
   const float x2 = x * x;  // |x| < 1/8: Taylor to x^7; the x^9 term is < 3e-10 |x| there
-  const float p = x * (1.f + x2 * (-0.333333333f + x2 * (0.133333333f + x2 * -0.0539682540f)));
-  const float t = 1.f - 2.f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(ax * 2.8853900817779268f) + 1.f);
-  return ax < 0.125f ? p : copysignf(t, x);
+  float p = x * (1.f + x2 * (-0.333333333f + x2 * (0.133333333f + x2 * -0.0539682540f)));
+  float t = copysignf(1.f - 2.f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(ax * 2.8853900817779268f) + 1.f), x);
+  asm("" : "+v"(p));
+  asm("" : "+v"(t));
+  return ax < 0.125f ? p : t;
 }
 __device__ __forceinline__ float elu_fast(float v) { return v < 0.f ? __expf(v) - 1.f : v; }
 __device__ __forceinline__ float act_f(float v, int act) {
@@ -95,11 +98,15 @@ __device__ __forceinline__ bool epi_skip(const GemmEpi& e) {
 // -log-likelihood term of one pixel, TF semantics log(y^x (1-y)^(1-x)) with pow(0,0) = 1 and
 // no epsilon (11a/vae.py:266-269). (A single-log form for binary targets makes hipcc spill
 // the wide kernel's accumulators across its main loop.)
+// Branch-free: both logs evaluated (pinned by the empty asm statements, else hipcc branches per
+// element around them) and each term selected, so a 0 * log(0) never enters the sum.
 __device__ __forceinline__ float bce_term(float yv, float xv) {
-  float term = 0.f;
-  if (xv != 0.f) term += xv * __logf(yv);
-  if (xv != 1.f) term += (1.f - xv) * __logf(1.f - yv);
-  return term;
+  float l1 = __logf(yv), l0 = __logf(1.f - yv);
+  asm("" : "+v"(l1));
+  asm("" : "+v"(l0));
+  const float a = xv != 0.f ? xv * l1 : 0.f;
+  const float b = xv != 1.f ? (1.f - xv) * l0 : 0.f;
+  return a + b;
 }
 
 // v -> n bf16 planes (n = 1: round to nearest; n = 3: exact split, each residual exact)
@@ -317,9 +324,55 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
   const int col0 = t.n0 + 8 * c8;
   const int nblk = (p.N + 127) / 128;
   const int gb = t.nt * (TW / 128) + (c8 >> 4);  // 128-column block of this chunk
+  constexpr int NQ = 64 / RP;                   // reader passes per band
+  // The operand each pass's math reads (DACT activation, BCE target) for all NQ passes of a
+  // band, loaded BEFORE the band's LDS transpose so their latency overlaps it (loading inside
+  // each pass exposed one global-load latency per pass: 16 per 256-row tile). bf16 sources
+  // stay packed (one uint4 per pass) until use.
+  constexpr bool LD = EPI == EPI_DACT || BCE;
+  auto pass_row = [&](int mi, int q) {
+    const int br = rr + RP * q;                                          // band row
+    return t.m0 + (br >> 5) * (MI * 32) + mi * 32 + (br & 31);           // tile row -> global
+  };
+  auto pass_nv = [&](int row) {
+    return row >= p.M ? 0 : (col0 >= p.N ? 0 : (p.N - col0 < 8 ? p.N - col0 : 8));
+  };
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi) {
     float* band = lds + (mi & 1) * BAND;
+    float sf[LD ? NQ : 1][8];   // fp32 operand (aux / target)
+    uint4 sb[LD ? NQ : 1];      // bf16 operand (auxp / target plane), packed
+    bool bsrc = false;          // the operand is bf16
+    if constexpr (LD) {
+      if constexpr (EPI == EPI_DACT) bsrc = e.auxp != nullptr;
+      if constexpr (EPI == EPI_BCEB) bsrc = true;
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) {
+        const int row = pass_row(mi, q);
+        const int nv = pass_nv(row);
+        int sr = row < p.M ? row : p.M - 1;
+        if constexpr (EPI == EPI_DACT) sr = sr >= e.remap_split ? sr - e.remap_shift : sr;
+        const int ld_src = EPI == EPI_DACT ? e.ld_aux : e.ldx;
+        if (bsrc) {
+          const unsigned short* src = (EPI == EPI_DACT ? e.auxp : e.xp) + (size_t)sr * ld_src + col0;
+          if (nv == 8) {
+            sb[q] = *reinterpret_cast<const uint4*>(src);
+          } else {
+            unsigned short h[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) h[j] = j < nv ? src[j] : (unsigned short)0;
+            sb[q] = make_uint4((unsigned)h[0] | (unsigned)h[1] << 16, (unsigned)h[2] | (unsigned)h[3] << 16,
+                               (unsigned)h[4] | (unsigned)h[5] << 16, (unsigned)h[6] | (unsigned)h[7] << 16);
+          }
+        } else {
+          const float* src = (EPI == EPI_DACT ? e.aux : e.x) + (size_t)sr * ld_src + col0;
+          if (nv == 8) ld8f(src, sf[q]);
+          else
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sf[q][j] = j < nv ? src[j] : 0.f;
+        }
+      }
+    }
     // writer: this wave's 32 x (TW/4) block of the band, C/D layout -> row-major
     if (!(diag & 4))
 #pragma unroll
@@ -331,55 +384,22 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
       }
     __syncthreads();
 #pragma unroll
-    for (int q = 0; q < 64 / RP; ++q) {
+    for (int q = 0; q < NQ; ++q) {
       const int br = rr + RP * q;                                    // band row
-      const int row = t.m0 + (br >> 5) * (MI * 32) + mi * 32 + (br & 31);  // tile row -> global
+      const int row = pass_row(mi, q);
       float v[8];
       const float4 a = *reinterpret_cast<const float4*>(band + br * TW + 8 * c8);
       const float4 b = *reinterpret_cast<const float4*>(band + br * TW + 8 * c8 + 4);
       v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
       const bool rok = row < p.M;
-      const bool full = rok && col0 + 8 <= p.N;
-      const int nv = !rok ? 0 : (col0 >= p.N ? 0 : (p.N - col0 < 8 ? p.N - col0 : 8));
+      const int nv = pass_nv(row);
+      const bool full = nv == 8;
       float rs = 0.f;
       if (nv > 0) {
         float sv[8];
-        if constexpr (EPI == EPI_DACT) {
-          const int ar = row >= e.remap_split ? row - e.remap_shift : row;
-          if (e.auxp) {  // the activation's bf16 plane (bf16 mode: no fp32 copy is written)
-            const unsigned short* src = e.auxp + (size_t)ar * e.ld_aux + col0;
-            if (full) {
-              const uint4 w = *reinterpret_cast<const uint4*>(src);
-              const unsigned ww[4] = {w.x, w.y, w.z, w.w};
-#pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                sv[2 * j] = __uint_as_float(ww[j] << 16);
-                sv[2 * j + 1] = __uint_as_float(ww[j] & 0xffff0000u);
-              }
-            } else {
-#pragma unroll
-              for (int j = 0; j < 8; ++j) sv[j] = j < nv ? bf16_bits_to_f32(src[j]) : 0.f;
-            }
-          } else {
-            const float* src = e.aux + (size_t)ar * e.ld_aux + col0;
-            if (full) ld8f(src, sv);
-            else
-#pragma unroll
-              for (int j = 0; j < 8; ++j) sv[j] = j < nv ? src[j] : 0.f;
-          }
-        }
-        if constexpr (EPI == EPI_BCE) {
-          const float* src = e.x + (size_t)row * e.ldx + col0;
-          if (full) ld8f(src, sv);
-          else
-#pragma unroll
-            for (int j = 0; j < 8; ++j) sv[j] = j < nv ? src[j] : 0.f;
-        }
-        if constexpr (EPI == EPI_BCEB) {
-          const unsigned short* src = e.xp + (size_t)row * e.ldx + col0;
-          if (full) {
-            const uint4 w = *reinterpret_cast<const uint4*>(src);
-            const unsigned ww[4] = {w.x, w.y, w.z, w.w};
+        if constexpr (LD) {
+          if (bsrc) {
+            const unsigned ww[4] = {sb[q].x, sb[q].y, sb[q].z, sb[q].w};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
               sv[2 * j] = __uint_as_float(ww[j] << 16);
@@ -387,18 +407,23 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
             }
           } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) sv[j] = j < nv ? bf16_bits_to_f32(src[j]) : 0.f;
+            for (int j = 0; j < 8; ++j) sv[j] = sf[q][j];
           }
         }
         float yv[8];
         if constexpr (BCE) {
+          if (diag & 8) {  // timing diagnostics: no transcendental math
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            if (diag & 8) { yv[j] = v[j]; rs += v[j] * sv[j]; v[j] = (yv[j] - sv[j]) * e.scale; continue; }
-            yv[j] = sigmoid_fast(v[j]);
-            // -log(y^x (1-y)^(1-x)) with TF pow(0,0) = 1 (no epsilon), 11a/vae.py:266-269
-            if (j < nv) rs += bce_term(yv[j], sv[j]);
-            v[j] = (yv[j] - sv[j]) * e.scale;
+            for (int j = 0; j < 8; ++j) { yv[j] = v[j]; rs += v[j] * sv[j]; v[j] = (yv[j] - sv[j]) * e.scale; }
+          } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              yv[j] = sigmoid_fast(v[j]);
+              // -log(y^x (1-y)^(1-x)) with TF pow(0,0) = 1 (no epsilon), 11a/vae.py:266-269
+              const float bt = bce_term(yv[j], sv[j]);
+              rs += j < nv ? bt : 0.f;
+              v[j] = (yv[j] - sv[j]) * e.scale;
+            }
           }
         }
         if constexpr (EPI == EPI_ACT)

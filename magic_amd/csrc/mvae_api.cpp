@@ -1500,6 +1500,9 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
     if (e == hipSuccess && np) {
       e = hipMalloc(&cpl, (size_t)np * nc * 2);
       d.epi.cp = cpl; d.epi.pc = (long long)nc; d.epi.ncp = np;
+      // MVAE_BENCH_PLANES_ONLY=1: the output as planes only, as the step's producers write it
+      if (const char* po = std::getenv("MVAE_BENCH_PLANES_ONLY"); po && *po == '1' && epi != EPI_BCE)
+        d.epi.c32 = 0;
     }
   }
   const size_t ws_n = gemm_workspace_elems(d);
