@@ -52,7 +52,8 @@ struct PParams {
   const int* dyn;                   // A residual planes nonzero? (nullptr: use all pairs)
   int diag;                         // timing diagnostics: bit 0 = no operand copies after the
                                     // prologue (the k-loop multiplies stale LDS images)
-  unsigned long long* stamps;       // twin kernel diagnostics build (ST): 4 stamps per workgroup
+  unsigned long long* stamps;       // stamped diagnostics builds (ST): 8 slots per workgroup
+                                    // {start, prologue landed, k-loop done, end, stores issued}
 };
 
 // 100 MHz constant-rate stamp, workgroup-comparable (diagnostics builds only)
@@ -602,7 +603,7 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
 
   const int np = (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
   const int nkt = t.ks < t.ke ? (t.ke - t.ks + BK - 1) / BK : 0;
-  const int total = np * nkt;
+  const int total = (pp.diag & 16) ? 0 : np * nkt;  // diag bit 4: the epilogue alone
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
   auto pa_of = [&](int pr) { return (pp.pab >> (4 * pr)) & 3; };
   auto pb_of = [&](int pr) { return (pp.pab >> (4 * pr + 2)) & 3; };
@@ -749,15 +750,17 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
     st2 = realtime();
     __builtin_amdgcn_sched_barrier(0);
   }
-  if constexpr (TE) epilogue_rm<EPI, 4, NI, 4, WNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag);
+  unsigned long long st_iss = 0;
+  if constexpr (TE) epilogue_rm<EPI, 4, NI, 4, WNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag,
+                                                    ST ? &st_iss : nullptr);
   else epilogue_g<EPI, 4, NI, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
   if constexpr (ST) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const unsigned long long st3 = realtime();
     if (threadIdx.x == 0) {
-      unsigned long long* o = pp.stamps + 4 * (size_t)blockIdx.x;
-      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3;
+      unsigned long long* o = pp.stamps + 8 * (size_t)blockIdx.x;
+      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = st_iss;
     }
   }
 }
@@ -910,15 +913,17 @@ __global__ __launch_bounds__(TNT, 2) void gemm_bf16t_kernel(PParams pp) {
     st2 = realtime();
     __builtin_amdgcn_sched_barrier(0);
   }
-  if constexpr (TE) epilogue_rm<EPI, 2, 2, 2, TNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag);
+  unsigned long long st_iss = 0;
+  if constexpr (TE) epilogue_rm<EPI, 2, 2, 2, TNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag,
+                                                    ST ? &st_iss : nullptr);
   else epilogue_g<EPI, 2, 2, TT, 2>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
   if constexpr (ST) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     const unsigned long long st3 = realtime();
     if (threadIdx.x == 0) {
-      unsigned long long* o = pp.stamps + 4 * (size_t)blockIdx.x;
-      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3;
+      unsigned long long* o = pp.stamps + 8 * (size_t)blockIdx.x;
+      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = st_iss;
     }
   }
 }

@@ -237,6 +237,7 @@ static void build_schedule(mvae_ctx* c) {
     GemmDesc d = gd(3 * B, c->enc[i].N, c->enc[i].K + 1, A, lda, false, th + c->enc[i].off,
                     c->enc[i].ld, false, c->H[i], c->ldh[i], EPI_ACT);
     d.epi.act = act;
+    d.epi.padw = 2;  // H[i]: the ones column at N, zeros beyond
     c->fwd_enc.push_back(d);
     c->fwd_enc_r.push_back(region(c, "enc_fwd_" + std::to_string(i)));
   }
@@ -253,9 +254,11 @@ static void build_schedule(mvae_ctx* c) {
   c->f_d1 = gd(B, c->d0, L + 1, c->z + (size_t)B * c->ldz, c->ldz, false, th + c->v1.off, c->v1.ld,
                false, c->a1, c->ld_d1, EPI_ACT);
   c->f_d1.epi.act = act;
+  c->f_d1.epi.padw = 2;
   c->f_d2 = gd(B, c->d1, c->d0 + 1, c->a1, c->ld_d1, false, th + c->v2.off, c->v2.ld, false, c->a2,
                c->ld_d2, EPI_ACT);
   c->f_d2.epi.act = act;
+  c->f_d2.epi.padw = 2;
   c->f_out = gd(B, c->D, c->d1 + 1, c->a2, c->ld_d2, false, th + c->vo.off, c->vo.ld, false, c->du,
                 c->ld_u, EPI_BCE);
   c->f_out.epi.x = c->xs + (size_t)B * c->ldx;
@@ -268,13 +271,13 @@ static void build_schedule(mvae_ctx* c) {
                           g1 + c->vo.off, c->vo.ld));
   GemmDesc dout = gd(B, c->d1, c->D, c->du, c->ld_u, false, th + c->vo.off, c->vo.ld, true, c->dzd2,
                      c->ld_d2, EPI_DACT);
-  dout.epi.act = act; dout.epi.aux = c->a2; dout.epi.ld_aux = c->ld_d2;
+  dout.epi.act = act; dout.epi.aux = c->a2; dout.epi.ld_aux = c->ld_d2; dout.epi.padw = 1;
   c->bwd_dec.push_back(dout);
   c->bwd_dec.push_back(gd(c->d0 + 1, c->d1, B, c->a1, c->ld_d1, true, c->dzd2, c->ld_d2, false,
                           g1 + c->v2.off, c->v2.ld));
   GemmDesc dd2 = gd(B, c->d0, c->d1, c->dzd2, c->ld_d2, false, th + c->v2.off, c->v2.ld, true, c->dzd1,
                     c->ld_d1, EPI_DACT);
-  dd2.epi.act = act; dd2.epi.aux = c->a1; dd2.epi.ld_aux = c->ld_d1;
+  dd2.epi.act = act; dd2.epi.aux = c->a1; dd2.epi.ld_aux = c->ld_d1; dd2.epi.padw = 1;
   c->bwd_dec.push_back(dd2);
   c->bwd_dec.push_back(gd(L + 1, c->d0, B, c->z + (size_t)B * c->ldz, c->ldz, true, c->dzd1,
                           c->ld_d1, false, g1 + c->v1.off, c->v1.ld));
@@ -296,6 +299,7 @@ static void build_schedule(mvae_ctx* c) {
                     c->lddz, EPI_DACT);
     d.epi.act = act; d.epi.aux = c->H[i - 1]; d.epi.ld_aux = c->ldh[i - 1];
     d.epi.remap_split = 2 * B; d.epi.remap_shift = B;
+    d.epi.padw = 1;  // dZ rows: zero padding
     c->bwd_enc.push_back(d);
     c->bwd_enc_r.push_back(region(c, head ? std::string("head_bwd_d") : "enc_bwd_d_" + std::to_string(i)));
   };
@@ -1464,7 +1468,7 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   d.variant = variant & 15;
   d.prec = (variant >> 4) & 15;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
   if (d.variant == 9) { d.valu = 1; d.prec = GEMM_F32; d.variant = 0; }  // the fp32 VALU kernel
-  d.diag = (variant >> 12) & 15; // kernel timing diagnostics (results meaningless)
+  d.diag = (variant >> 12) & 31; // kernel timing diagnostics (results meaningless)
   unsigned short* planes = nullptr;
   const int np = d.prec == GEMM_F32 ? 0 : (d.prec == GEMM_BF16 ? 1 : 3);
   hipError_t e = hipMalloc(&A, na * 4);
@@ -1497,6 +1501,7 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
     d.epi.x = aux; d.epi.ldx = ldc;
     d.epi.rowpart = rowpart;
     d.epi.scale = 1.f / M;
+    if (epi == EPI_ACT || epi == EPI_DACT) d.epi.padw = 1;  // as the step's padded rows
     if (e == hipSuccess && np) {
       e = hipMalloc(&cpl, (size_t)np * nc * 2);
       d.epi.cp = cpl; d.epi.pc = (long long)nc; d.epi.ncp = np;
@@ -1523,29 +1528,32 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   if (const char* sp = std::getenv("MVAE_STAMPS"); e == hipSuccess && sp && *sp == '1') {
     const int nmax = 1 << 20;
     unsigned long long* sb = nullptr;
-    e = hipMalloc(&sb, (size_t)4 * nmax * 8);
-    if (e == hipSuccess) e = hipMemsetAsync(sb, 0, (size_t)4 * nmax * 8, st);
+    e = hipMalloc(&sb, (size_t)8 * nmax * 8);
+    if (e == hipSuccess) e = hipMemsetAsync(sb, 0, (size_t)8 * nmax * 8, st);
     GemmDesc ds = d;
     ds.stamps = sb;
     if (e == hipSuccess) e = gemm_run(ds, ws, ws_n, st);
     if (e == hipSuccess) e = hipStreamSynchronize(st);
-    std::vector<unsigned long long> h((size_t)4 * nmax);
+    std::vector<unsigned long long> h((size_t)8 * nmax);
     if (e == hipSuccess) e = hipMemcpy(h.data(), sb, h.size() * 8, hipMemcpyDeviceToHost);
     if (sb) (void)hipFree(sb);
     int n = 0;
     unsigned long long lo = ~0ull, hi = 0;
-    double seg[3] = {0, 0, 0};
+    double seg[3] = {0, 0, 0}, iss = 0;
+    int niss = 0;
     for (int i = 0; i < nmax && e == hipSuccess; ++i) {
-      const unsigned long long* q = &h[4 * (size_t)i];
+      const unsigned long long* q = &h[8 * (size_t)i];
       if (!q[0]) continue;
       ++n;
       lo = std::min(lo, q[0]); hi = std::max(hi, q[3]);
       for (int k = 0; k < 3; ++k) seg[k] += (double)(q[k + 1] - q[k]) * 0.01;
+      if (q[4]) { iss += (double)(q[4] - q[2]) * 0.01; ++niss; }
     }
+    if (niss) std::fprintf(stderr, "[stamps] epilogue stores issued after %.2f us (mean of %d WGs)\n", iss / niss, niss);
     if (n) {
       std::vector<double> st0s, ends;
       for (int i = 0; i < nmax; ++i) {
-        const unsigned long long* q = &h[4 * (size_t)i];
+        const unsigned long long* q = &h[8 * (size_t)i];
         if (!q[0]) continue;
         st0s.push_back((q[0] - lo) * 0.01);
         ends.push_back((q[3] - lo) * 0.01);

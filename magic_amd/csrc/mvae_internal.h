@@ -50,6 +50,11 @@ struct GemmEpi {
   long long pc = 0;
   int ncp = 0;
   int c32 = 1;                  // 0: no fp32 C store (every consumer reads the planes)
+  // Row padding [N, round8(N)) of the output and of the DACT / BCE operand rows (all strides
+  // multiples of 8) may be read and written as whole 8-column chunks, the padding written with
+  // its constant value: 1.0 at column N when padw == 2 (an activation's ones column), else 0.
+  // (Element-wise stores of a partial last chunk cost ~5 us per 256x256-tile epilogue.)
+  int padw = 0;
 };
 
 // bf16 operand shadows (precision = bf16). When set, the GEMM reads A/B from these
