@@ -751,8 +751,12 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
     __builtin_amdgcn_sched_barrier(0);
   }
   unsigned long long st_iss = 0;
+  // BCE row partials in the LDS past the two 64-row bands (2 x 64 x TN floats): 32 KB of 160
+  // (TN 256) or 64 KB of 128 (TN 128), 256 x TN / 8 floats needed
+  static_assert(2 * 64 * TN * 4 + 256 * (TN / 8) * 4 <= (3 * IMA + 2 * IMB) * 2, "BCE partials LDS");
   if constexpr (TE) epilogue_rm<EPI, 4, NI, 4, WNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag,
-                                                    ST ? &st_iss : nullptr);
+                                                    ST ? &st_iss : nullptr,
+                                                    reinterpret_cast<float*>(smem) + 2 * 64 * TN);
   else epilogue_g<EPI, 4, NI, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
   if constexpr (ST) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -768,7 +772,9 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
 template <bool AT, bool BT, int EPI, bool TE, int TN>
 hipError_t launch_q(const PParams& p, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
-  if constexpr (EPI == EPI_ACT && TE && !AT && !BT) {  // stamped diagnostics build (bench only)
+  // stamped diagnostics builds (bench only): the hidden forward (ACT), the BCE head (BCEB, bf16 binary target as in the step) and
+  // the hidden dgrad (DACTB: bf16 aux, B = W^T)
+  if constexpr (TE && !AT && ((EPI == EPI_ACT && !BT) || (EPI == EPI_BCEB && !BT) || (EPI == EPI_DACTB && BT))) {
     if (p.stamps) {
       hipLaunchKernelGGL((gemm_bf16q_kernel<AT, BT, EPI, TE, TN, true>), dim3(nwg), dim3(WNT), 0, st, p);
       return hipGetLastError();
@@ -1167,7 +1173,9 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
     switch (epi) {
       case EPI_STORE: return launch_wide<EPI_STORE>(p, d.at, d.bt, d.variant, st);
       case EPI_ACT: return launch_wide<EPI_ACT>(p, d.at, d.bt, d.variant, st);
-      case EPI_DACT: return launch_wide<EPI_DACT>(p, d.at, d.bt, d.variant, st);
+      case EPI_DACT:
+        return d.epi.auxp ? launch_wide<EPI_DACTB>(p, d.at, d.bt, d.variant, st)
+                          : launch_wide<EPI_DACT>(p, d.at, d.bt, d.variant, st);
       case EPI_BCE: return launch_wide<EPI_BCE>(p, d.at, d.bt, d.variant, st);
       case EPI_BCEB: return launch_wide<EPI_BCEB>(p, d.at, d.bt, d.variant, st);
       case EPI_SIGMOID: return launch_wide<EPI_SIGMOID>(p, d.at, d.bt, d.variant, st);

@@ -25,20 +25,26 @@ struct Params {
 };
 constexpr int TN_TWIN = 1;  // Params::tn of the 128 x 128 twin kernel (gemm_bf16.hip)
 
-// tanh from the hardware exp / reciprocal (v_exp_f32, v_rcp_f32) and an odd polynomial where
-// 1 - 2/(e^2x + 1) cancels: relative error < 2e-6 everywhere (the accurate tanhf costs ~50 VALU
-// instructions per element, which the hidden-layer epilogues could not hide)
-// (branch-free: both forms are evaluated and one selected by v_cndmask -- the empty asm
-// statements pin both values, otherwise hipcc turns the select into a per-element exec-mask
-// branch around the exp / rcp, which made the epilogue several times slower)
+// tanh as an odd [13/6] rational in x on [-7.905, 7.905] (clamped beyond, where tanh rounds to
+// +-1): one v_rcp_f32 and FMAs that pair into packed v_pk_fma_f32, relative error < 6e-7
+// everywhere (numpy check against float64 tanh on a 2M-point grid, tools/micro/README). The
+// previous exp/reciprocal form (two transcendentals plus a Taylor branch near 0) kept the
+// hidden-layer epilogues VALU-bound: the quarter-rate transcendentals dominate their math.
 __device__ __forceinline__ float tanh_fast(float x) {
-  const float ax = fabsf(x);
-  const float x2 = x * x;  // |x| < 1/8: Taylor to x^7; the x^9 term is < 3e-10 |x| there
-  float p = x * (1.f + x2 * (-0.333333333f + x2 * (0.133333333f + x2 * -0.0539682540f)));
-  float t = copysignf(1.f - 2.f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(ax * 2.8853900817779268f) + 1.f), x);
-  asm("" : "+v"(p));
-  asm("" : "+v"(t));
-  return ax < 0.125f ? p : t;
+  const float c = __builtin_amdgcn_fmed3f(x, -7.90531110763549805f, 7.90531110763549805f);
+  const float x2 = c * c;
+  float p = fmaf(x2, -2.76076847742355e-16f, 2.00018790482477e-13f);
+  p = fmaf(x2, p, -8.60467152213735e-11f);
+  p = fmaf(x2, p, 5.12229709037114e-08f);
+  p = fmaf(x2, p, 1.48572235717979e-05f);
+  p = fmaf(x2, p, 6.37261928875436e-04f);
+  p = fmaf(x2, p, 4.89352455891786e-03f);
+  float q = fmaf(x2, 1.19825839466702e-06f, 1.18534705686654e-04f);
+  q = fmaf(x2, q, 2.26843463243900e-03f);
+  q = fmaf(x2, q, 4.89352518554385e-03f);
+  float r = (p * c) * __builtin_amdgcn_rcpf(q);
+  asm("" : "+v"(r));  // pinned: the NaN select below stays a v_cndmask, not a branch
+  return x != x ? x : r;  // NaN propagates (the clamp would map it to +-1)
 }
 __device__ __forceinline__ float elu_fast(float v) { return v < 0.f ? __expf(v) - 1.f : v; }
 __device__ __forceinline__ float act_f(float v, int act) {
@@ -76,6 +82,10 @@ __device__ __forceinline__ float sigmoid_f(float v) { return 1.f / (1.f + expf(-
 __device__ __forceinline__ float sigmoid_fast(float v) {
   return __builtin_amdgcn_rcpf(1.f + __expf(-v));
 }
+
+// the dgrad epilogue (fp32 aux or its bf16 plane)
+template <int EPI>
+constexpr bool is_dact = EPI == EPI_DACT || EPI == EPI_DACTB;
 
 // bijective XCD remap: consecutive logical tiles land on the same XCD (blockIdx % 8 group)
 __device__ __forceinline__ int xcd_remap(int b, int nwg) {
@@ -168,9 +178,9 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
   // (Interleaving load -> use -> store per element serialises one memory latency per element:
   // the stores may alias the loads.)
   constexpr bool BCE = EPI == EPI_BCE || EPI == EPI_BCEB;
-  constexpr bool READS = EPI == EPI_DACT || BCE;
-  const float* __restrict__ src = EPI == EPI_DACT ? e.aux : e.x;
-  const int lds_ = EPI == EPI_DACT ? e.ld_aux : e.ldx;
+  constexpr bool READS = is_dact<EPI> || BCE;
+  const float* __restrict__ src = is_dact<EPI> ? e.aux : e.x;
+  const int lds_ = is_dact<EPI> ? e.ld_aux : e.ldx;
   // not unrolled: the block's accumulators are acc[0], rotated down after each block (one copy
   // of the epilogue code, see epilogue_rm)
 #pragma unroll 1
@@ -181,13 +191,13 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
       for (int r = 0; r < 16; ++r) {
         const int row = rbase + mi * 32 + (r & 3) + 8 * (r >> 2);
         int sr = row < p.M ? row : p.M - 1;
-        if constexpr (EPI == EPI_DACT) sr = sr >= e.remap_split ? sr - e.remap_shift : sr;
+        if constexpr (is_dact<EPI>) sr = sr >= e.remap_split ? sr - e.remap_shift : sr;
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
           int col = cbase + ni * 32;
           col = col < p.N ? col : p.N - 1;
           if constexpr (EPI == EPI_BCEB) sv[r][ni] = bf16_bits_to_f32(e.xp[(size_t)sr * lds_ + col]);
-          else if constexpr (EPI == EPI_DACT)
+          else if constexpr (is_dact<EPI>)
             sv[r][ni] = e.auxp ? bf16_bits_to_f32(e.auxp[(size_t)sr * lds_ + col]) : src[(size_t)sr * lds_ + col];
           else sv[r][ni] = src[(size_t)sr * lds_ + col];
         }
@@ -196,7 +206,7 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
     // ACT / DACT: the activation over the block's 16 x NI values with the act switch hoisted
     // out of the element loop (per-element runtime selects broke the epilogue into branches)
     float av[16 * NI];
-    if constexpr (EPI == EPI_ACT || EPI == EPI_DACT) {
+    if constexpr (EPI == EPI_ACT || is_dact<EPI>) {
 #pragma unroll
       for (int r = 0; r < 16; ++r)
 #pragma unroll
@@ -222,7 +232,7 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
         if (row < p.M && col < p.N) {
           const size_t o = (size_t)row * p.ldc + col;
           float v = acc[0][ni][r];
-          if constexpr (EPI == EPI_ACT || EPI == EPI_DACT) v = av[r * NI + ni];
+          if constexpr (EPI == EPI_ACT || is_dact<EPI>) v = av[r * NI + ni];
           if constexpr (BCE) {
             const float yv = sigmoid_fast(v);
             const float xv = sv[r][ni];
@@ -314,10 +324,15 @@ __device__ __forceinline__ void st8_planes(unsigned short* cp, long long pc, int
 // accumulator row block mi of both wave rows (64 rows); `lds` holds two bands (2 x 64 x TW fp32).
 // Wide kernels: MI 4, NWN 4, NTH 512 (256 x 128*NI tiles); twin kernel: 2, 2, 2, 256 (128 x 128).
 // issued (stamped diagnostics builds only): s_memrealtime once the last store is issued
+// rpl (BCE): LDS for the per-chunk row partials, (64 MI) x (TW / 8) floats past the two band
+// buffers; nullptr: a 16-lane xor-shuffle tree per pass instead (its four dependent lane
+// exchanges behind each pass's transcendentals measured ~9 us per 256x256 tile,
+// tools/micro/epi.hip)
 template <int EPI, int MI, int NI, int NWN, int NTH>
 __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x16 (&acc)[MI][NI],
                                             float* lds, int wm, int wn, int diag = 0,
-                                            unsigned long long* issued = nullptr) {
+                                            unsigned long long* issued = nullptr,
+                                            float* rpl = nullptr) {
   constexpr int TW = NWN * NI * 32, BAND = 64 * TW;  // band row width, floats per band buffer
   static_assert(TW % 128 == 0, "BCE row partials are per 128-column block");
   constexpr int CW = TW / 8;                    // 8-column chunks per band row
@@ -337,7 +352,7 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
   // band, loaded BEFORE the band's LDS transpose so their latency overlaps it (loading inside
   // each pass exposed one global-load latency per pass: 16 per 256-row tile). bf16 sources
   // stay packed (one uint4 per pass) until use.
-  constexpr bool LD = EPI == EPI_DACT || BCE;
+  constexpr bool LD = is_dact<EPI> || BCE;
   auto pass_row = [&](int mi, int q) {
     const int br = rr + RP * q;                                          // band row
     return t.m0 + (br >> 5) * (MI * 32) + mi * 32 + (br & 31);           // tile row -> global
@@ -347,27 +362,19 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
   };
   // whole-chunk access of a partial last chunk (GemmEpi::padw)
   auto pass_full = [&](int nv) { return nv == 8 || (e.padw && nv > 0); };
-  // One band per iteration of a NON-unrolled loop: the band's accumulators are always acc[0]
-  // (the blocks rotate down after the writer), so the epilogue code is emitted once instead of
-  // MI times (37.6 -> 13.6 KB for the 256x256 ACT kernel; no time change measured).
-#pragma unroll 1
-  for (int mi = 0; mi < MI; ++mi) {
-    float* band = lds + (mi & 1) * BAND;
-    float sf[LD ? NQ : 1][8];   // fp32 operand (aux / target)
-    uint4 sb[LD ? NQ : 1];      // bf16 operand (auxp / target plane), packed
-    bool bsrc = false;          // the operand is bf16
+  constexpr bool bsrc = EPI == EPI_DACTB || EPI == EPI_BCEB;  // the operand is bf16
+  // the operand rows of band mi's NQ passes: bf16 packed into sb (b16) or fp32 into sf
+  auto load_band = [&](int mi, bool b16, float (&sf)[LD ? NQ : 1][8], uint4 (&sb)[LD ? NQ : 1]) {
     if constexpr (LD) {
-      if constexpr (EPI == EPI_DACT) bsrc = e.auxp != nullptr;
-      if constexpr (EPI == EPI_BCEB) bsrc = true;
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
         const int row = pass_row(mi, q);
         const int nv = pass_nv(row);
         int sr = row < p.M ? row : p.M - 1;
-        if constexpr (EPI == EPI_DACT) sr = sr >= e.remap_split ? sr - e.remap_shift : sr;
-        const int ld_src = EPI == EPI_DACT ? e.ld_aux : e.ldx;
-        if (bsrc) {
-          const unsigned short* src = (EPI == EPI_DACT ? e.auxp : e.xp) + (size_t)sr * ld_src + col0;
+        if constexpr (is_dact<EPI>) sr = sr >= e.remap_split ? sr - e.remap_shift : sr;
+        const int ld_src = is_dact<EPI> ? e.ld_aux : e.ldx;
+        if (b16) {
+          const unsigned short* src = (is_dact<EPI> ? e.auxp : e.xp) + (size_t)sr * ld_src + col0;
           if (pass_full(nv)) {
             sb[q] = *reinterpret_cast<const uint4*>(src);
           } else {
@@ -378,13 +385,31 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
                                (unsigned)h[4] | (unsigned)h[5] << 16, (unsigned)h[6] | (unsigned)h[7] << 16);
           }
         } else {
-          const float* src = (EPI == EPI_DACT ? e.aux : e.x) + (size_t)sr * ld_src + col0;
+          const float* src = (is_dact<EPI> ? e.aux : e.x) + (size_t)sr * ld_src + col0;
           if (pass_full(nv)) ld8f(src, sf[q]);
           else
 #pragma unroll
             for (int j = 0; j < 8; ++j) sf[q][j] = j < nv ? src[j] : 0.f;
         }
       }
+    }
+  };
+  // bf16 operands are loaded one band ahead (issued before band mi-1's transpose and passes),
+  // so their latency hides behind a whole band of work; fp32 operands (twice the registers:
+  // double-buffered they spill) at the start of their own band, before its LDS transpose
+  float sf[LD ? NQ : 1][8];
+  uint4 sb[LD ? NQ : 1], sbn[LD ? NQ : 1];
+  if (bsrc) load_band(0, true, sf, sb);
+  // One band per iteration of a NON-unrolled loop: the band's accumulators are always acc[0]
+  // (the blocks rotate down after the writer), so the epilogue code is emitted once instead of
+  // MI times (37.6 -> 13.6 KB for the 256x256 ACT kernel; no time change measured).
+#pragma unroll 1
+  for (int mi = 0; mi < MI; ++mi) {
+    float* band = lds + (mi & 1) * BAND;
+    if (bsrc) {
+      if (mi + 1 < MI) load_band(mi + 1, true, sf, sbn);
+    } else {
+      load_band(mi, false, sf, sb);
     }
     // writer: this wave's 32 x (TW/4) block of the band, C/D layout -> row-major
     if (!(diag & 4))
@@ -434,13 +459,32 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
             for (int j = 0; j < 8; ++j) { yv[j] = v[j]; rs += v[j] * sv[j]; v[j] = (yv[j] - sv[j]) * e.scale; }
           } else {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              yv[j] = sigmoid_fast(v[j]);
-              // -log(y^x (1-y)^(1-x)) with TF pow(0,0) = 1 (no epsilon), 11a/vae.py:266-269
-              const float bt = bce_term(yv[j], sv[j]);
-              rs += j < nv ? bt : 0.f;
-              v[j] = (yv[j] - sv[j]) * e.scale;
+            for (int j = 0; j < 8; ++j) yv[j] = sigmoid_fast(v[j]);
+            // binary targets (every target of the wave's passes 0 or 1, a wave-uniform branch):
+            // the term is log(x ? y : 1 - y) -- the same value as the two-log form below, whose
+            // other term is exactly 0 -- at one logarithm per pixel instead of two
+            // (hardware log2 scaled by ln 2: v_log_f32 + one multiply, where __logf expands to
+            // ~12 instructions of denormal scaling and extended-precision correction)
+            bool bin = true;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) bin &= (sv[j] == 0.f) | (sv[j] == 1.f);
+            if (__all(bin)) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const float bt = __builtin_amdgcn_logf(sv[j] != 0.f ? yv[j] : 1.f - yv[j]) *
+                                 0.693147180559945309f;
+                rs += j < nv ? bt : 0.f;
+              }
+            } else {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                // -log(y^x (1-y)^(1-x)) with TF pow(0,0) = 1 (no epsilon), 11a/vae.py:266-269
+                const float bt = bce_term(yv[j], sv[j]);
+                rs += j < nv ? bt : 0.f;
+              }
             }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = (yv[j] - sv[j]) * e.scale;
           }
         }
         if constexpr (EPI == EPI_ACT)
@@ -449,7 +493,7 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
 #pragma unroll
           for (int j = 0; j < 8; ++j) v[j] = sigmoid_f(v[j]);
         }
-        if constexpr (EPI == EPI_DACT) dact_n(v, sv, e.act);
+        if constexpr (is_dact<EPI>) dact_n(v, sv, e.act);
         if (nv < 8) {  // padding columns of a whole-chunk store (GemmEpi::padw)
 #pragma unroll
           for (int j = 0; j < 8; ++j)
@@ -476,9 +520,45 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
         }
       }
       if constexpr (BCE) {
+        if (rpl) {
+          rpl[(br >> 5) * (MI * 32 * CW) + (mi * 32 + (br & 31)) * CW + c8] = rs;
+        } else {
 #pragma unroll
-        for (int off = 8; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
-        if ((c8 & 15) == 0 && rok && gb < nblk) e.rowpart[(size_t)row * nblk + gb] = -rs;
+          for (int off = 8; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
+          if ((c8 & 15) == 0 && rok && gb < nblk) e.rowpart[(size_t)row * nblk + gb] = -rs;
+        }
+      }
+    }
+    if constexpr (LD) {
+#pragma unroll
+      for (int q = 0; q < NQ; ++q) sb[q] = sbn[q];
+    }
+  }
+  if constexpr (BCE) {
+    if (rpl) {
+      // each (tile row, 128-column block): its 16 chunk partials summed in the order of the
+      // xor-shuffle tree (off = 8, 4, 2, 1 -- the same sums, bit for bit)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      constexpr int NB = TW / 128;
+      for (int i = tid; i < 64 * MI * NB; i += NTH) {
+        const int tr = i / NB, b = i - tr * NB;
+        const int row = t.m0 + tr, gbb = t.nt * NB + b;
+        const float* q = rpl + tr * CW + 16 * b;
+        float v[16];
+#pragma unroll
+        for (int j = 0; j < 16; j += 4) {
+          const float4 a = *reinterpret_cast<const float4*>(q + j);
+          v[j] = a.x; v[j + 1] = a.y; v[j + 2] = a.z; v[j + 3] = a.w;
+        }
+        float t8[8], t4[4];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t8[j] = v[j] + v[j + 8];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t4[j] = t8[j] + t8[j + 4];
+        const float sum = (t4[0] + t4[2]) + (t4[1] + t4[3]);
+        if (row < p.M && gbb < nblk) e.rowpart[(size_t)row * nblk + gbb] = -sum;
       }
     }
   }

@@ -1489,7 +1489,7 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   // output planes the next GEMM would read
   const int epi = (variant >> 8) & 15;
   float *aux = nullptr, *rowpart = nullptr;
-  unsigned short* cpl = nullptr;
+  unsigned short *cpl = nullptr, *xpl = nullptr;
   if (e == hipSuccess && epi != EPI_STORE) {
     if (epi > EPI_SIGMOID) e = hipErrorInvalidValue;
     d.epi.mode = epi;
@@ -1505,9 +1505,19 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
     if (e == hipSuccess && np) {
       e = hipMalloc(&cpl, (size_t)np * nc * 2);
       d.epi.cp = cpl; d.epi.pc = (long long)nc; d.epi.ncp = np;
-      // MVAE_BENCH_PLANES_ONLY=1: the output as planes only, as the step's producers write it
-      if (const char* po = std::getenv("MVAE_BENCH_PLANES_ONLY"); po && *po == '1' && epi != EPI_BCE)
+      // MVAE_BENCH_PLANES_ONLY=1: the output as planes only, as the step's producers write it;
+      // the BCE head as in the step: binary targets read from their bf16 plane (EPI_BCEB)
+      if (const char* po = std::getenv("MVAE_BENCH_PLANES_ONLY"); po && *po == '1') {
         d.epi.c32 = 0;
+        if (epi == EPI_BCE && e == hipSuccess) {
+          e = launch_binarize(aux, (size_t)M * ldc, st);
+          if (e == hipSuccess) e = hipMalloc(&xpl, (size_t)M * ldc * 2 + 16);
+          if (e == hipSuccess) e = launch_split_planes(aux, (size_t)M * ldc, Planes{xpl, 0, 1}, st);
+          if (e == hipSuccess) e = hipMemsetAsync(reinterpret_cast<char*>(xpl) + (size_t)M * ldc * 2, 0, 16, st);
+          d.epi.xp = xpl;
+          d.epi.xdyn = reinterpret_cast<const int*>(reinterpret_cast<char*>(xpl) + (size_t)M * ldc * 2);
+        }
+      }
     }
   }
   const size_t ws_n = gemm_workspace_elems(d);
@@ -1571,6 +1581,7 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   for (float* p : {A, Bm, Cm, ws, aux, rowpart}) if (p) (void)hipFree(p);
   if (planes) (void)hipFree(planes);
   if (cpl) (void)hipFree(cpl);
+  if (xpl) (void)hipFree(xpl);
   if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
   return MVAE_OK;
 }

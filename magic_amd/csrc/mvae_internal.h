@@ -16,6 +16,9 @@ enum EpiMode {
   EPI_BCEB = 5,     // EPI_BCE reading the target from its bf16 plane (kernel-internal: gemm_run
                     // launches EPI_BCE and EPI_BCEB and each returns at once unless *xdyn
                     // selects it -- a runtime choice inside one epilogue spills the accumulators)
+  EPI_DACTB = 6,    // EPI_DACT reading aux from its bf16 plane auxp (kernel-internal: the wide
+                    // bf16 kernels' instantiation when auxp is set, so the fp32-aux path and its
+                    // registers are not compiled into it)
 };
 
 enum Act { ACT_TANH = 0, ACT_ELU = 1 };
@@ -148,6 +151,8 @@ struct AdamArgs {
 };
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
 hipError_t launch_split_planes(const float* src, size_t n, const Planes& dst, hipStream_t st);
+// x[i] = x[i] > 0 ? 1 : 0 (diagnostics: binary BCE targets for the GEMM harness)
+hipError_t launch_binarize(float* x, size_t n, hipStream_t st);
 hipError_t launch_make_batch(const unsigned char* locks, const unsigned char* keys, int H, int W,
                              const int* idx, const float* coef, int B, float div, float* x,
                              hipStream_t st);

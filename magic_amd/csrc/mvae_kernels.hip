@@ -730,6 +730,17 @@ hipError_t launch_split_planes(const float* src, size_t n, const Planes& dst, hi
   return hipGetLastError();
 }
 
+__global__ void binarize_kernel(float* x, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) x[i] = x[i] > 0.f ? 1.f : 0.f;
+}
+
+hipError_t launch_binarize(float* x, size_t n, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(binarize_kernel, dim3(nblocks(n, 256)), dim3(256), 0, st, x, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_make_batch(const unsigned char* locks, const unsigned char* keys, int H, int W,
                              const int* idx, const float* coef, int B, float div, float* x,
                              hipStream_t st) {

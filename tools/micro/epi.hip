@@ -12,9 +12,12 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ unsigned short bf(float v) { return __builtin_bit_cast(unsigned short, __float2bfloat16(v)); }
 
-// flags: 1 LDS writer + barrier, 2 LDS reads, 4 partial last chunk (N = 500), 8 tanh-ish math
+// flags: 1 LDS writer + barrier, 2 LDS reads, 4 partial last chunk (N = 500), 8 tanh-ish math,
+// 16 a bf16 operand row per pass (loaded at band start), 32 BCE math (sigmoid, one log, dU),
+// 64 BCE row partial (xor-shuffle tree + 4-B store per 16 lanes)
 template <int FL>
-__global__ __launch_bounds__(512, 1) void epi(unsigned short* out, int ld, int N, int M, float seed) {
+__global__ __launch_bounds__(512, 1) void epi(unsigned short* out, int ld, int N, int M, float seed,
+                                               const unsigned short* x, float* rowpart) {
   __shared__ __attribute__((aligned(16))) float lds[2 * 64 * 256];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, wm = wave >> 2, wn = wave & 3;
   const int ntn = 2, b = blockIdx.x, m0 = (b / ntn) * 256, n0 = (b % ntn) * 256;
@@ -27,6 +30,15 @@ __global__ __launch_bounds__(512, 1) void epi(unsigned short* out, int ld, int N
 #pragma unroll 1
   for (int mi = 0; mi < 4; ++mi) {
     float* band = lds + (mi & 1) * 64 * 256;
+    uint4 xb[4];
+    if constexpr (FL & 16) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int br = rr + 16 * q;
+        const int row = m0 + (br >> 5) * 128 + mi * 32 + (br & 31);
+        xb[q] = *reinterpret_cast<const uint4*>(x + (size_t)row * ld + col0);
+      }
+    }
     if constexpr (FL & 1) {
       for (int ni = 0; ni < 2; ++ni)
         for (int r = 0; r < 16; ++r) {
@@ -52,6 +64,23 @@ __global__ __launch_bounds__(512, 1) void epi(unsigned short* out, int ld, int N
       if constexpr (FL & 8) {
         for (int j = 0; j < 8; ++j) v[j] = 1.f - 2.f * __builtin_amdgcn_rcpf(__builtin_amdgcn_exp2f(v[j] * 2.885f) + 1.f);
       }
+      float rs = 0.f;
+      if constexpr (FL & 32) {
+        float sv[8];
+        const unsigned ww[4] = {xb[q].x, xb[q].y, xb[q].z, xb[q].w};
+        for (int j = 0; j < 4; ++j) { sv[2 * j] = __uint_as_float(ww[j] << 16); sv[2 * j + 1] = __uint_as_float(ww[j] & 0xffff0000u); }
+        for (int j = 0; j < 8; ++j) {
+          const float y = __builtin_amdgcn_rcpf(1.f + __expf(-v[j]));
+          rs += __logf(sv[j] != 0.f ? y : 1.f - y);
+          v[j] = (y - sv[j]) * 1e-4f;
+        }
+      } else if constexpr (FL & 16) {
+        v[0] += __uint_as_float(xb[q].x);
+      }
+      if constexpr (FL & 64) {
+        for (int off = 8; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
+        if ((c8 & 15) == 0) rowpart[(size_t)row * 4 + (c8 >> 4)] = -rs;
+      }
       const int nv = row >= M ? 0 : (col0 >= N ? 0 : (N - col0 < 8 ? N - col0 : 8));
       unsigned short* o = out + (size_t)row * ld + col0;
       if (nv == 8) {
@@ -66,14 +95,15 @@ __global__ __launch_bounds__(512, 1) void epi(unsigned short* out, int ld, int N
 }
 
 template <int FL>
-static void run(const char* name, unsigned short* out, int N) {
+static void run(const char* name, unsigned short* out, int N, const unsigned short* x = nullptr,
+                float* rp = nullptr) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
   const int M = 24576, nwg = 192, ld = 504;
-  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(epi<FL>, dim3(nwg), dim3(512), 0, 0, out, ld, N, M, 0.5f);
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(epi<FL>, dim3(nwg), dim3(512), 0, 0, out, ld, N, M, 0.5f, x, rp);
   CK(hipEventRecord(a));
   const int it = 20;
-  for (int w = 0; w < it; ++w) hipLaunchKernelGGL(epi<FL>, dim3(nwg), dim3(512), 0, 0, out, ld, N, M, 0.5f);
+  for (int w = 0; w < it; ++w) hipLaunchKernelGGL(epi<FL>, dim3(nwg), dim3(512), 0, 0, out, ld, N, M, 0.5f, x, rp);
   CK(hipEventRecord(b));
   CK(hipEventSynchronize(b));
   float ms; CK(hipEventElapsedTime(&ms, a, b));
@@ -90,5 +120,13 @@ int main() {
   run<7>("+ partial chunk", out, 500);
   run<15>("+ math", out, 500);
   run<11>("writer+reads+math, no partial", out, 512);
+  unsigned short* x; float* rp;
+  CK(hipMalloc(&x, (size_t)24576 * 504 * 2));
+  CK(hipMemset(x, 0, (size_t)24576 * 504 * 2));
+  CK(hipMalloc(&rp, (size_t)24576 * 4 * 4));
+  run<3 | 2 | 16>("writer+reads + operand loads", out, 512, x, rp);
+  run<3 | 2 | 16 | 32>("+ BCE math", out, 512, x, rp);
+  run<3 | 2 | 16 | 32 | 64>("+ BCE row partials", out, 512, x, rp);
+  run<3 | 2 | 16 | 64>("operand + row partials, no BCE math", out, 512, x, rp);
   return 0;
 }
