@@ -604,6 +604,9 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   const int np = (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
   const int nkt = t.ks < t.ke ? (t.ke - t.ks + BK - 1) / BK : 0;
   const int total = (pp.diag & 16) ? 0 : np * nkt;  // diag bit 4: the epilogue alone
+  // s_setprio 1 around each k16-step's MFMAs (cdna_hip_programming.md T5): +1-3 % on the step's
+  // GEMMs, +3-7 % on 4096^3 (profiles/r3/gemm_ab_setprio_r3u.txt); diag bit 5 turns it off (A/B)
+  const bool sprio = (pp.diag & 32) == 0;
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
   auto pa_of = [&](int pr) { return (pp.pab >> (4 * pr)) & 3; };
   auto pb_of = [&](int pr) { return (pp.pab >> (4 * pr + 2)) & 3; };
@@ -690,6 +693,7 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
       const int cur = ks & 1, nx = cur ^ 1;
       wait_lds<0>();  // this step's fragments (read during the previous step's MFMAs)
       __builtin_amdgcn_sched_barrier(0);
+      if (sprio) __builtin_amdgcn_s_setprio(1);
       if (ks + 1 < KS) {
         // MFMA i, then the fragments of step ks+1 assigned to its gap
 #pragma unroll
@@ -740,6 +744,8 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
           __builtin_amdgcn_sched_barrier(0);
         }
       }
+      if (sprio) __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
     }
     // KS is even: the next iteration's step 0 reads land in fa/fb[0]
   }

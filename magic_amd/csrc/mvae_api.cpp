@@ -1468,7 +1468,7 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   d.variant = variant & 15;
   d.prec = (variant >> 4) & 15;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
   if (d.variant == 9) { d.valu = 1; d.prec = GEMM_F32; d.variant = 0; }  // the fp32 VALU kernel
-  d.diag = (variant >> 12) & 31; // kernel timing diagnostics (results meaningless)
+  d.diag = (variant >> 12) & 63; // kernel timing diagnostics (results meaningless; 32: A/B switch)
   unsigned short* planes = nullptr;
   const int np = d.prec == GEMM_F32 ? 0 : (d.prec == GEMM_BF16 ? 1 : 3);
   hipError_t e = hipMalloc(&A, na * 4);
