@@ -563,6 +563,12 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16r_kernel(PParams pp) {
 // Tile 256 x TN (TN = 256 or 128), 8 waves 2 (M) x 4 (N), each 128 x TN/4 = 4 x NI 32x32
 // accumulators. TN = 128 doubles the tile count of a narrow GEMM (N ~ 500: the hidden encoder
 // and decoder layers) so it fills the chip without split-K slabs and their reduction.
+// MVAE_QGAP (build-time A/B): the next k16-step's fragment reads are spread over the first
+// NM - MVAE_QGAP MFMA gaps, so the last one has MVAE_QGAP more MFMAs to land before the step's
+// lgkmcnt(0)
+#ifndef MVAE_QGAP
+#define MVAE_QGAP 0
+#endif
 template <bool AT, bool BT, int EPI, bool TE, int TN, bool ST = false>
 __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   constexpr int BK = 64;
@@ -702,7 +708,7 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
           __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
           for (int f = 0; f < NF; ++f)
-            if (f * NM / NF == i) rd_f(sa, sb, ks + 1, f, nx);
+            if (f * (NM - MVAE_QGAP) / NF == i) rd_f(sa, sb, ks + 1, f, nx);
           __builtin_amdgcn_sched_barrier(0);
         }
       } else {
