@@ -329,6 +329,15 @@ __device__ __forceinline__ void wait_dma(int tiles) {
   }
 }
 
+// wait until at most N vector-memory operations are outstanding (N literal per instantiation)
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  if constexpr (N == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else if constexpr (N == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 // BK: k-tile depth; DEPTH LDS stages, the copy of tile it + DEPTH - 1 issued while tile it is
 // multiplied. DEPTH 2 waits for the next tile's copy at every barrier (vmcnt(0)); deeper
 // pipelines keep DEPTH - 2 copies in flight across the barrier, which therefore is a raw
@@ -569,14 +578,18 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16r_kernel(PParams pp) {
 #ifndef MVAE_QGAP
 #define MVAE_QGAP 0
 #endif
-template <bool AT, bool BT, int EPI, bool TE, int TN, bool ST = false>
+// MI = 3 (k-contiguous A only): a 192 x TN tile (each wave 96 x TN/4), so a 3B-row GEMM of
+// 24576 rows is 128 x 2 = 256 workgroups -- one per CU -- instead of 96 x 2 = 192 (256 rows).
+template <bool AT, bool BT, int EPI, bool TE, int TN, int MI = 4, bool ST = false>
 __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   constexpr int BK = 64;
   constexpr int NI = TN / 128;
-  constexpr int IMA = WT * BK, IMB = TN * BK;  // bf16 elements per operand image
+  constexpr int TM = 64 * MI;                  // tile rows: 2 wave rows x MI 32-row blocks
+  static_assert(MI == 4 || (MI == 3 && !AT), "192-row tiles need a k-contiguous A operand");
+  constexpr int IMA = TM * BK, IMB = TN * BK;  // bf16 elements per operand image
   constexpr int KS = BK / 16;
-  constexpr int NM = 4 * NI;                   // MFMAs per wave per k16-step
-  constexpr int NF = NI + 4;                   // fragments per wave per k16-step (B first)
+  constexpr int NM = MI * NI;                  // MFMAs per wave per k16-step
+  constexpr int NF = NI + MI;                  // fragments per wave per k16-step (B first)
   const Params& p = pp.g;
   if (epi_skip<EPI>(p.epi)) return;
   unsigned long long st0 = 0, st1 = 0, st2 = 0;
@@ -585,23 +598,27 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
     st0 = realtime();
     __builtin_amdgcn_sched_barrier(0);
   }
-  __shared__ __attribute__((aligned(16))) short smem[3 * IMA + 2 * IMB];  // A slots | B slots
+  // A ring slots | B ring slots; the row-major epilogue's two 64-row bands (and the BCE row
+  // partials) reuse it after the k-loop
+  constexpr int RING = 3 * IMA + 2 * IMB;
+  constexpr int EPIL = TE ? 2 * (2 * 64 * TN + 64 * MI * (TN / 8)) : 0;
+  __shared__ __attribute__((aligned(16))) short smem[RING > EPIL ? RING : EPIL];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
-  const Tile t = tile_of_t<WT, TN>(p, true);
+  const Tile t = tile_of_t<TM, TN>(p, true);
   const unsigned short* __restrict__ A = pp.A + t.bi * p.sA;
   const unsigned short* __restrict__ Bm = pp.B + t.bi * p.sB;
 
-  WLoad<!AT, BK> la;
+  WLoad<!AT, BK, TM> la;
   WLoad<BT, BK, TN> lb;
   la.init(p.lda, t.m0, p.M, wave, lane);
   lb.init(p.ldb, t.n0, p.N, wave, lane);
 
-  f32x16 acc[4][NI];
+  f32x16 acc[MI][NI];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < NI; ++j)
 #pragma unroll
@@ -622,7 +639,7 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   int bkt = 0, bpr = 0, ib = 0, bsl = 0;
   bool pend_a = false;  // the A copy issued with the last B copy (vmcnt accounting)
   const bool dma = !(pp.diag & 1);
-  constexpr int GA = WLoad<!AT, BK>::NG;  // DMA instructions per A image per thread
+  constexpr int GA = WLoad<!AT, BK, TM>::NG;  // DMA instructions per A image per thread
   // move the A cursor to ia+1 and copy its image if it differs from ia's
   auto next_a = [&]() -> bool {
     if (ia + 1 >= total || !dma) return false;
@@ -648,9 +665,9 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   int sa_q[3] = {0, 0, 0};
   int sb_q[2] = {0, 0};
 
-  bf16x8 fa[2][4], fb[2][NI];
+  bf16x8 fa[2][MI], fb[2][NI];
   auto rd_a = [&](int slot, int ks, int mi, bf16x8& a) {
-    a = la.frag(smem + slot * IMA, lds0 + 2u * (unsigned)(slot * IMA), wm * 128 + mi * 32, ks, lane);
+    a = la.frag(smem + slot * IMA, lds0 + 2u * (unsigned)(slot * IMA), wm * (MI * 32) + mi * 32, ks, lane);
   };
   auto rd_b = [&](int slot, int ks, int ni, bf16x8& b) {
     b = lb.frag(smem + 3 * IMA + slot * IMB, lds0 + 2u * (unsigned)(3 * IMA + slot * IMB),
@@ -673,8 +690,7 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
     const bool a1 = next_a();
     sa_q[0] = 0; sa_q[1] = asl;
     if (a1) {
-      if constexpr (GA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      wait_vm<GA>();
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -720,8 +736,7 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
           // images of it+1 landed (only the A copy issued after its B copy may be in flight),
           // every wave's reads of it's images are done: its freed slots can be refilled
           if (pend_a) {
-            if constexpr (GA == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-            else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+            wait_vm<GA>();
           } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           }
@@ -763,13 +778,12 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
     __builtin_amdgcn_sched_barrier(0);
   }
   unsigned long long st_iss = 0;
-  // BCE row partials in the LDS past the two 64-row bands (2 x 64 x TN floats): 32 KB of 160
-  // (TN 256) or 64 KB of 128 (TN 128), 256 x TN / 8 floats needed
-  static_assert(2 * 64 * TN * 4 + 256 * (TN / 8) * 4 <= (3 * IMA + 2 * IMB) * 2, "BCE partials LDS");
-  if constexpr (TE) epilogue_rm<EPI, 4, NI, 4, WNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag,
-                                                    ST ? &st_iss : nullptr,
-                                                    reinterpret_cast<float*>(smem) + 2 * 64 * TN);
-  else epilogue_g<EPI, 4, NI, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
+  // BCE row partials in the LDS past the two 64-row bands (2 x 64 x TN floats), 64 MI x TN / 8
+  // floats (EPIL above)
+  if constexpr (TE) epilogue_rm<EPI, MI, NI, 4, WNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag,
+                                                     ST ? &st_iss : nullptr,
+                                                     reinterpret_cast<float*>(smem) + 2 * 64 * TN);
+  else epilogue_g<EPI, MI, NI, TM, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
   if constexpr (ST) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -781,23 +795,29 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   }
 }
 
-template <bool AT, bool BT, int EPI, bool TE, int TN>
+template <bool AT, bool BT, int EPI, bool TE, int TN, int MI = 4>
 hipError_t launch_q(const PParams& p, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
   // stamped diagnostics builds (bench only): the hidden forward (ACT), the BCE head (BCEB, bf16 binary target as in the step) and
   // the hidden dgrad (DACTB: bf16 aux, B = W^T)
   if constexpr (TE && !AT && ((EPI == EPI_ACT && !BT) || (EPI == EPI_BCEB && !BT) || (EPI == EPI_DACTB && BT))) {
     if (p.stamps) {
-      hipLaunchKernelGGL((gemm_bf16q_kernel<AT, BT, EPI, TE, TN, true>), dim3(nwg), dim3(WNT), 0, st, p);
+      hipLaunchKernelGGL((gemm_bf16q_kernel<AT, BT, EPI, TE, TN, MI, true>), dim3(nwg), dim3(WNT), 0, st, p);
       return hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((gemm_bf16q_kernel<AT, BT, EPI, TE, TN>), dim3(nwg), dim3(WNT), 0, st, p);
+  hipLaunchKernelGGL((gemm_bf16q_kernel<AT, BT, EPI, TE, TN, MI>), dim3(nwg), dim3(WNT), 0, st, p);
   return hipGetLastError();
 }
 
 template <int EPI, bool TE, int TN>
 hipError_t launch_q_l(const PParams& p, bool at, bool bt, hipStream_t st) {
+  // 192-row tiles (planner: Params::tm == 192) for the A-k-contiguous non-BCE epilogues
+  constexpr bool T192 = EPI != EPI_BCE && EPI != EPI_BCEB && EPI != EPI_SIGMOID;
+  if constexpr (T192) {
+    if (p.g.tm == 192 && !at)
+      return bt ? launch_q<false, true, EPI, TE, TN, 3>(p, st) : launch_q<false, false, EPI, TE, TN, 3>(p, st);
+  }
   if (!at && !bt) return launch_q<false, false, EPI, TE, TN>(p, st);
   if (at && !bt) return launch_q<true, false, EPI, TE, TN>(p, st);
   if (!at && bt) return launch_q<false, true, EPI, TE, TN>(p, st);
@@ -1112,7 +1132,15 @@ bool gemm_bf16_wide(const GemmDesc& d) {
 // of resident workgroups x (k-tiles + fixed prologue/epilogue cost) x its time per k-tile;
 // split-K adds the fp32 slab round trip and the reduction launch. Variants 11 / 12 force the
 // ring kernel at tile N 128 / 256, 13 / 14 the twin kernel, 15 the ring kernels only.
-struct WidePlan { int split = 1; int tn = 256; };
+struct WidePlan { int split = 1; int tn = 256; int tm = 256; };
+// MVAE_TM192=0 (A/B): plan the ring kernels at 256-row tiles only
+static bool tm192_enabled() {
+  static const bool on = [] {
+    const char* v = std::getenv("MVAE_TM192");
+    return !(v && *v == '0');
+  }();
+  return on;
+}
 static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
   const bool fixed = d.epi.mode == EPI_BCE || d.epi.mode == EPI_BCEB || d.epi.mode == EPI_SIGMOID;
   const int kt = (d.K + 63) / 64;
@@ -1124,20 +1152,28 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
   const bool big = d.M >= 256 && d.N >= 256;
   double best = 1e30;
   WidePlan pl;
-  for (int w : {256, 128, TN_TWIN}) {
+  // 192-row ring tiles: k-contiguous A, epilogues other than the BCE head / sigmoid
+  const bool t192 = tm192_enabled() && !d.at && d.epi.mode != EPI_BCE && d.epi.mode != EPI_BCEB &&
+                    d.epi.mode != EPI_SIGMOID;
+  for (int cand = 0; cand < 5; ++cand) {
+    // candidates: ring 256x256, 256x128, twin 128x128, ring 192x256, 192x128
+    const int w = cand == 0 || cand == 3 ? 256 : cand == 1 || cand == 4 ? 128 : TN_TWIN;
+    const int tmr = cand >= 3 ? 192 : 256;
     const bool twin = w == TN_TWIN;
+    if (cand >= 3 && !t192) continue;
     if (d.variant == 11 && w != 128) continue;
     if (d.variant == 12 && w != 256) continue;
     if ((d.variant == 13 || d.variant == 14) && !twin) continue;
     if (d.variant == 15 && twin) continue;
     if (!twin && !big && d.variant != 3 && d.variant < 5) continue;
-    const int tm = twin ? TT : WT, tnn = twin ? TT : w;
+    const int tm = twin ? TT : tmr, tnn = twin ? TT : w;
     const long long tiles = (long long)((d.M + tm - 1) / tm) * ((d.N + tnn - 1) / tnn) * d.batch;
     // ring kernels, measured: 4096^3 at 1.06 PF/s = 1.94 us per 256x256 k-tile per CU; the
-    // 256x128 tile does half the MFMA work per k-tile in ~1.5 us (profiles/r2/gemm_ab_tile_n.txt).
+    // 256x128 tile does half the MFMA work per k-tile in ~1.5 us (profiles/r2/gemm_ab_tile_n.txt);
+    // 192-row tiles interpolated (a fixed ~1.1 us per k-tile plus ~0.1 us per 32x32 block).
     // twin: two resident 128x128 workgroups per CU, t_kt per k-tile of one of them, epilogue
     // and prologue mostly hidden behind the co-resident workgroup
-    const double t_kt = twin ? 0.55e-6 : (w == 256 ? 1.9e-6 : 1.5e-6);
+    const double t_kt = twin ? 0.55e-6 : tmr == 192 ? (w == 256 ? 1.7e-6 : 1.4e-6) : (w == 256 ? 1.9e-6 : 1.5e-6);
     const double slots = twin ? 512.0 : 256.0;
     const double fix = twin ? 1.5 : 3.0;
     for (int s = 1; s <= (fixed ? 1 : 32); ++s) {
@@ -1146,7 +1182,7 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
       const double rounds = std::ceil(tiles * s / slots);
       double t = rounds * (np * std::ceil((double)kt / s) + fix) * t_kt * (twin ? 2.0 : 1.0);
       if (s > 1) t += (double)d.batch * s * d.M * d.N * 8.0 / 4.5e12 + 4e-6;
-      if (t < best * 0.97) { best = t; pl.split = s; pl.tn = w; }
+      if (t < best * 0.97) { best = t; pl.split = s; pl.tn = w; pl.tm = twin ? TT : tmr; }
     }
   }
   return pl;
@@ -1155,6 +1191,8 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
 int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws) { return wide_plan(d, max_ws).split; }
 
 int gemm_bf16_wide_tn(const GemmDesc& d, size_t max_ws) { return wide_plan(d, max_ws).tn; }
+
+int gemm_bf16_wide_tm(const GemmDesc& d, size_t max_ws) { return wide_plan(d, max_ws).tm; }
 
 hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, hipStream_t st) {
   PParams p;
@@ -1179,7 +1217,8 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
     // tile N: the planner's (gemm_run), 256 for the diagnostic variants of the 256x256 forms
     const bool q = d.variant == 0 || d.variant == 3 || (d.variant >= 10 && d.variant <= 15);
     p.g.tn = q && (g.tn == 128 || g.tn == TN_TWIN) ? g.tn : 256;
-    const int tm = p.g.tn == TN_TWIN ? TT : WT, tn = p.g.tn == TN_TWIN ? TT : p.g.tn;
+    p.g.tm = q && p.g.tn != TN_TWIN && g.tm == 192 && !d.at ? 192 : 256;
+    const int tm = p.g.tn == TN_TWIN ? TT : p.g.tm, tn = p.g.tn == TN_TWIN ? TT : p.g.tn;
     p.g.ntm = (d.M + tm - 1) / tm;
     p.g.ntn = (d.N + tn - 1) / tn;
     switch (epi) {

@@ -21,6 +21,7 @@ struct Params {
   int batch, split, kchunk;
   int ntm, ntn;
   int tn;                   // bf16 DMA kernels: ring-kernel tile N (256 or 128) or TN_TWIN
+  int tm = 256;             // ... and ring-kernel tile M (256, or 192 for a k-contiguous A)
   GemmEpi epi;
 };
 constexpr int TN_TWIN = 1;  // Params::tn of the 128 x 128 twin kernel (gemm_bf16.hip)

@@ -383,6 +383,7 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   const int split = d.split > 0 ? d.split : gemm_plan_split(d, ws ? ws_elems : 0);
   p.split = split;
   p.tn = gemm_bf16_wide(d) ? gemm_bf16_wide_tn(d, ws ? ws_elems : 0) : 0;
+  p.tm = gemm_bf16_wide(d) ? gemm_bf16_wide_tm(d, ws ? ws_elems : 0) : 256;
   const int kb = d.prec == GEMM_F32 ? BK : 64;  // k-tile of the kernel that runs
   const int ktiles = (d.K + kb - 1) / kb;
   p.kchunk = ((ktiles + split - 1) / split) * kb;

@@ -720,9 +720,9 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     auto show = [&](const GemmDesc& d, int r) {
       const int sp = gemm_plan_split(d, ws);
       const bool wide = gemm_bf16_wide(d);
-      std::fprintf(stderr, "[mvae plan] %-16s M %6d N %6d K %6d batch %d prec %d valu %d wide %d tile_n %d split %d\n",
+      std::fprintf(stderr, "[mvae plan] %-16s M %6d N %6d K %6d batch %d prec %d valu %d wide %d tile %dx%d split %d\n",
                    r >= 0 ? c->region_names[r].c_str() : "?", d.M, d.N, d.K, d.batch, d.prec, d.valu,
-                   (int)wide, wide ? gemm_bf16_wide_tn(d, ws) : 0, sp);
+                   (int)wide, wide ? gemm_bf16_wide_tm(d, ws) : 0, wide ? gemm_bf16_wide_tn(d, ws) : 0, sp);
     };
     for (size_t i = 0; i < c->fwd_enc.size(); ++i) show(c->fwd_enc[i], c->fwd_enc_r[i]);
     show(c->f_d1, c->f_d1_r); show(c->f_d2, c->f_d2_r); show(c->f_out, c->f_out_r);

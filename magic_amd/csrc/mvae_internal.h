@@ -100,6 +100,8 @@ hipError_t gemm_valu_launch(const gemm::Params& p, const GemmDesc& d, int epi, h
 int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws);
 // tile N (256 or 128) of the wide kernel for d (the same plan as gemm_bf16_wide_split)
 int gemm_bf16_wide_tn(const GemmDesc& d, size_t max_ws);
+// ... and its tile M (256, or 192: k-contiguous A, not the BCE head)
+int gemm_bf16_wide_tm(const GemmDesc& d, size_t max_ws);
 // Number of column blocks the BCE epilogue writes per row (rowpart's inner dim).
 int gemm_bce_nblk(int N);
 
