@@ -333,7 +333,14 @@ __global__ void latent_fwd_kernel(const float* __restrict__ ms, EpsSrc es, float
 // mode 0 (colsq):  out[j] = sum_b z_lock[b][j]^2 (j < L), sum_b z_key[b][j-L]^2 (j >= L)
 // mode 1 (coldot): out[i] = sum_b draw_b * n_lock[b][i] * n_key[b][i]
 // Two-stage, fixed-order (deterministic): partials over row chunks, then chunk sums.
-constexpr int CS_ROWS = 128;
+// Column statistics of the cosine metric in two fixed-order passes: chunk partials of CS_ROWS
+// rows (4 row lanes x CS_ROWS / 4 rows each, their loads issued before the ordered sum), then
+// the ordered sum over chunks. (With 128-row chunks every thread waited out 32 dependent
+// global loads in a row and the final pass another nchunk: 20-30 us per statistic for a few
+// hundred KB.)
+constexpr int CS_ROWS = 32;
+constexpr int CS_PER = CS_ROWS / 4;  // rows per thread
+
 __global__ void colstats_part_kernel(int mode, const float* __restrict__ z, int B, int L, int ldz,
                                      const float* __restrict__ colsq, const float* __restrict__ draw,
                                      float* __restrict__ part) {
@@ -341,23 +348,33 @@ __global__ void colstats_part_kernel(int mode, const float* __restrict__ z, int 
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 cols x 4 row lanes
   const int j = blockIdx.x * 64 + tx;
   const int r0 = blockIdx.y * CS_ROWS;
-  const int r1 = min(B, r0 + CS_ROWS);
   __shared__ float red[4][64];
   float acc = 0.f;
   if (j < ncols) {
     if (mode == 0) {
       const float* src = j < L ? z + (size_t)B * ldz + j : z + (size_t)2 * B * ldz + (j - L);
-      for (int b = r0 + ty; b < r1; b += 4) {
-        const float v = src[(size_t)b * ldz];
-        acc += v * v;
+      float v[CS_PER];
+#pragma unroll
+      for (int i = 0; i < CS_PER; ++i) {
+        const int b = r0 + ty + 4 * i;
+        v[i] = b < B ? src[(size_t)b * ldz] : 0.f;
       }
+#pragma unroll
+      for (int i = 0; i < CS_PER; ++i) acc += v[i] * v[i];
     } else {
       const float rl = rsqrtf(fmaxf(colsq[j], L2_EPS));
       const float rk = rsqrtf(fmaxf(colsq[L + j], L2_EPS));
-      for (int b = r0 + ty; b < r1; b += 4) {
-        const float zl = z[(size_t)(B + b) * ldz + j], zk = z[(size_t)(2 * B + b) * ldz + j];
-        acc += draw[b] * (zl * rl) * (zk * rk);
+      float zl[CS_PER], zk[CS_PER], dr[CS_PER];
+#pragma unroll
+      for (int i = 0; i < CS_PER; ++i) {
+        const int b = r0 + ty + 4 * i;
+        const bool ok = b < B;
+        zl[i] = ok ? z[(size_t)(B + b) * ldz + j] : 0.f;
+        zk[i] = ok ? z[(size_t)(2 * B + b) * ldz + j] : 0.f;
+        dr[i] = ok ? draw[b] : 0.f;
       }
+#pragma unroll
+      for (int i = 0; i < CS_PER; ++i) acc += dr[i] * (zl[i] * rl) * (zk[i] * rk);
     }
   }
   red[ty][tx] = acc;
@@ -371,7 +388,15 @@ __global__ void colstats_final_kernel(const float* __restrict__ part, int nchunk
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= ncols) return;
   float acc = 0.f;
-  for (int c = 0; c < nchunk; ++c) acc += part[(size_t)c * ncols + j];
+  int c = 0;
+  for (; c + 8 <= nchunk; c += 8) {  // 8 loads in flight, summed in chunk order
+    float t[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[i] = part[(size_t)(c + i) * ncols + j];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc += t[i];
+  }
+  for (; c < nchunk; ++c) acc += part[(size_t)c * ncols + j];
   out[j] = acc;
 }
 
