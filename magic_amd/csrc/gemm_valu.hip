@@ -98,6 +98,29 @@ __global__ __launch_bounds__(VNT) void gemm_valu_kernel(Params p) {
   const bool alb = ((reinterpret_cast<uintptr_t>(Bm) & 15) | (p.ldb & 3)) == 0;
   VStage<!AT> la;
   VStage<BT> lb;
+  // DACT: this thread's 4 x 4 activation values loaded before the k-loop, their latency behind
+  // it (loaded in the epilogue, each row's loads waited behind the previous row's stores, which
+  // may alias them)
+  float ax[4][4];
+  if constexpr (EPI == EPI_DACT) {
+    const GemmEpi& e = p.epi;
+    const int c0 = t.n0 + 4 * tn;
+    const bool av = c0 + 4 <= p.N && (e.ld_aux & 3) == 0 && (reinterpret_cast<uintptr_t>(e.aux) & 15) == 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int row = t.m0 + 4 * tm + i;
+      row = row < p.M ? row : p.M - 1;
+      const int ar = row >= e.remap_split ? row - e.remap_shift : row;
+      const float* x = e.aux + (size_t)ar * e.ld_aux + c0;
+      if (av) {
+        const float4 q = *reinterpret_cast<const float4*>(x);
+        ax[i][0] = q.x; ax[i][1] = q.y; ax[i][2] = q.z; ax[i][3] = q.w;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ax[i][j] = c0 + j < p.N ? x[j] : 0.f;
+      }
+    }
+  }
   const int nch = t.ks < t.ke ? (t.ke - t.ks + VKC - 1) / VKC : 0;
   if (nch > 0) {
     la.load(A, p.lda, t.m0, p.M, t.ks, t.ke, tid, ala);
@@ -153,10 +176,8 @@ __global__ __launch_bounds__(VNT) void gemm_valu_kernel(Params p) {
       for (int j = 0; j < 4; ++j) v[j] = sigmoid_f(v[j]);
     }
     if constexpr (EPI == EPI_DACT) {
-      const int ar = row >= e.remap_split ? row - e.remap_shift : row;
-      const float* x = e.aux + (size_t)ar * e.ld_aux;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) v[j] = c0 + j < p.N ? dact_f(v[j], x[c0 + j], e.act) : 0.f;
+      for (int j = 0; j < 4; ++j) v[j] = c0 + j < p.N ? dact_f(v[j], ax[i][j], e.act) : 0.f;
     }
     const size_t o = (size_t)row * p.ldc + c0;
     if (vec) {
