@@ -1161,6 +1161,7 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
     const int tmr = cand >= 3 ? 192 : 256;
     const bool twin = w == TN_TWIN;
     if (cand >= 3 && !t192) continue;
+    if ((d.tm == 192 && t192 && cand != 3 && cand != 4) || (d.tm == 256 && cand >= 3)) continue;
     if (d.variant == 11 && w != 128) continue;
     if (d.variant == 12 && w != 256) continue;
     if ((d.variant == 13 || d.variant == 14) && !twin) continue;

@@ -1326,6 +1326,7 @@ extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int
   d.prec = (epi >> 4) & 15;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
   d.variant = (epi >> 8) & 15;
   if (d.variant == 9) { d.valu = 1; d.prec = GEMM_F32; d.variant = 0; }  // the fp32 VALU kernel
+  if ((epi >> 13) & 1) d.tm = 192;  // epi bit 13: the ring kernel's 192-row tiles where eligible
   d.epi.act = act;
   d.epi.aux = aux;
   d.epi.ld_aux = ld_aux;

@@ -77,6 +77,7 @@ struct GemmDesc {
   int split = 0;                       // forced split-K (0 = planner)
   int diag = 0;                        // kernel timing diagnostics (gemm_bf16.hip PParams::diag)
   int valu = 0;                        // 1: the fp32 VALU kernel (gemm_valu.hip; skinny shapes)
+  int tm = 0;                          // ring-kernel tile M forced (tests): 192 or 256; 0 = planner
   // diagnostics build of the twin kernel (mvae_bench_gemm, MVAE_STAMPS=1): per workgroup
   // s_memrealtime stamps {start, prologue copy landed, k-loop done, end} (never in the step)
   unsigned long long* stamps = nullptr;

@@ -163,6 +163,33 @@ class TangoEncoder(object):
         self.engine.close()
 
 
+def sample_latent_space(vae, nx: int = 20, ny: int = 20, lo: float = -3.0, hi: float = 3.0):
+    """The 2-D latent-space sampling grid of ``11a/utils.py:401-422`` as an array (the reference
+    plots it to a PNG; plotting is out of scope): an (ny*S) x (nx*S) canvas, S = image side, tile
+    (nx - i - 1, j) = ``vae.generate`` of z = (v[j], v[i]) with v = linspace(lo, hi, nx), as the
+    reference's loop over ``yi in x_values`` / ``xi in y_values`` places it. The reference runs one
+    ``generate`` per grid point on a batch of identical rows and keeps row 0; here the grid points
+    are the rows of ``ceil(nx*ny / batch_size)`` batched ``generate`` calls. Returns None unless
+    the latent space is 2-D (the reference prints a message instead).
+    """
+    if vae.latent_dimensions != 2:
+        return None
+    x_values = np.linspace(lo, hi, nx)
+    y_values = np.linspace(lo, hi, ny)
+    z = np.array([[xi, yi] for yi in x_values for xi in y_values], dtype=np.float32)
+    rows = []
+    for s0 in range(0, len(z), vae.batch_size):
+        rows.append(np.asarray(vae.generate(z[s0:s0 + vae.batch_size])))
+    imgs = np.concatenate(rows, axis=0)
+    side = int(round(np.sqrt(imgs.shape[1])))
+    canvas = np.empty((side * ny, side * nx), dtype=imgs.dtype)
+    for i in range(len(x_values)):
+        for j in range(len(y_values)):
+            canvas[(nx - i - 1) * side:(nx - i) * side, j * side:(j + 1) * side] = \
+                imgs[i * len(y_values) + j].reshape(side, side)
+    return canvas
+
+
 def cosine_distance(a, b):
     """``11a/vae.py:444-458``: l2-normalise along axis 0 (the batch axis), then the row-wise
     dot product. Host helper (numpy) for tools and tests; the step computes this in HIP."""

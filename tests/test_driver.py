@@ -109,3 +109,39 @@ def test_keyboard_interrupt_is_swallowed():
 
     out, hist = train(vae, gen(), 24, training_epochs=3, log=lambda s: None)
     assert out is vae and len(vae.fit_calls) == 4  # 4 steps + the eval dequeue at i == 3
+
+
+def test_sample_latent_space_grid_layout():
+    """11a/utils.py:401-422: tile (nx-i-1, j) holds generate(z = (v[j], v[i])); batched calls of
+    at most batch_size rows (host logic, a stand-in generate that encodes z in its pixels)."""
+    import numpy as np
+    from magic_amd.vae import sample_latent_space
+
+    class Fake:
+        latent_dimensions = 2
+        batch_size = 7
+        calls = []
+
+        def generate(self, z):
+            z = np.asarray(z)
+            assert 1 <= len(z) <= self.batch_size
+            self.calls.append(len(z))
+            img = np.zeros((len(z), 16), dtype=np.float32)
+            img[:, 0] = z[:, 0]
+            img[:, 1] = z[:, 1]
+            return img
+
+    f = Fake()
+    c = sample_latent_space(f, nx=5, ny=5)
+    assert c.shape == (20, 20)
+    v = np.linspace(-3, 3, 5)
+    for i in range(5):
+        for j in range(5):
+            tile = c[(5 - i - 1) * 4:(5 - i) * 4, j * 4:(j + 1) * 4].reshape(-1)
+            assert tile[0] == np.float32(v[j]) and tile[1] == np.float32(v[i])
+    assert sum(f.calls) == 25 and max(f.calls) == 7
+
+    class Fake3(Fake):
+        latent_dimensions = 3
+
+    assert sample_latent_space(Fake3()) is None

@@ -158,3 +158,56 @@ def test_wgrad0_chunks_tile_grads_and_match_backward(chunks, prec, conv):
             eng.set_option("wgrad0_chunks", 3)
     finally:
         eng.close()
+
+
+# ------------------------------------------------------------------ 192-row ring tiles
+@pytest.mark.parametrize("prec", [2, 1], ids=["f32x", "bf16"])
+@pytest.mark.parametrize("bt", [0, 1])
+@pytest.mark.parametrize("M,N,K,mode", [(192, 256, 64, 0), (193, 500, 501, 1), (1000, 600, 4099, 0),
+                                        (600, 130, 300, 1), (385, 517, 1001, 2), (24576 // 8, 500, 501, 1)])
+def test_gemm_tile192(bt, M, N, K, mode, prec):
+    """epi bit 13 forces the ring kernel's 192-row tiles (MI = 3, k-contiguous A): ragged M / N /
+    K edges, the planner's split-K (K 4099), and the ACT / DACT epilogues (mode 1 / 2)."""
+    lib = _lib.load()
+    g = torch.Generator(device="cuda").manual_seed(M * 13 + N * 7 + K + mode)
+    A = _padded(M, K, g)
+    Bm = _padded(N, K, g) if bt else _padded(K, N, g)
+    aux = torch.rand(M, (N + 7) // 8 * 8, device="cuda", generator=g) * 1.6 - 0.8
+    C = torch.full((M, N), float("nan"), device="cuda")
+    rc = lib.mvae_debug_gemm(M, N, K, A.data_ptr(), A.shape[1], 0, Bm.data_ptr(), Bm.shape[1], bt,
+                             C.data_ptr(), N, mode | (prec << 4) | (1 << 13), 0,
+                             aux.data_ptr() if mode == 2 else None, aux.shape[1],
+                             torch.cuda.current_stream().cuda_stream)
+    assert rc == 0, lib.mvae_last_error(None)
+    Ad = A[:, :K].double()
+    Bd = Bm[:, :K].double().T if bt else Bm[:, :N].double()
+    ref = Ad @ Bd
+    mag = (Ad.abs() @ Bd.abs()).max().item()
+    if mode == 1:
+        ref = torch.tanh(ref)
+    elif mode == 2:
+        y = aux[:, :N].double()
+        ref = ref * (1 - y * y)
+    err = (C.double() - ref).abs().max().item()
+    bound = (2e-6 if prec != 1 else 1e-2) * mag + 1e-6
+    assert err <= bound, (err, bound)
+
+
+def test_sample_latent_space_gpu():
+    """11a/utils.py:401-422 on the GPU decoder: every tile of the batched canvas equals a
+    single-row generate of its grid point (L = 2, preset 11a at 20 x 20, batch 8)."""
+    import numpy as np
+    from magic_amd.vae import TangoEncoder, sample_latent_space
+    cfg = preset("11a", image_size=20, batch=8)
+    cfg.latent = 2
+    vae = TangoEncoder(None, config=cfg)
+    try:
+        c = sample_latent_space(vae, nx=4, ny=4)
+        assert c.shape == (80, 80) and np.isfinite(c).all()
+        v = np.linspace(-3, 3, 4)
+        for i, j in [(0, 0), (1, 3), (3, 2)]:
+            one = vae.generate(np.array([[v[j], v[i]]], dtype=np.float32))[0].reshape(20, 20)
+            tile = c[(4 - i - 1) * 20:(4 - i) * 20, j * 20:(j + 1) * 20]
+            np.testing.assert_allclose(tile, one, rtol=0, atol=1e-6)
+    finally:
+        vae.close()
