@@ -592,7 +592,7 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
   constexpr int NF = NI + MI;                  // fragments per wave per k16-step (B first)
   const Params& p = pp.g;
   if (epi_skip<EPI>(p.epi)) return;
-  unsigned long long st0 = 0, st1 = 0, st2 = 0;
+  unsigned long long st0 = 0, st1 = 0, st2 = 0, st_wait = 0, st_vmw = 0;
   if constexpr (ST) {
     __builtin_amdgcn_sched_barrier(0);
     st0 = realtime();
@@ -733,6 +733,8 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
         __builtin_amdgcn_sched_barrier(0);
         const bool more = it + 1 < total;
         if (more) {
+          unsigned long long tw0 = 0;
+          if constexpr (ST) tw0 = realtime();
           // images of it+1 landed (only the A copy issued after its B copy may be in flight),
           // every wave's reads of it's images are done: its freed slots can be refilled
           if (pend_a) {
@@ -740,8 +742,14 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
           } else {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
           }
+          if constexpr (ST) {  // stamped builds: time in the vmcnt wait, then in the barrier
+            const unsigned long long tw1 = realtime();
+            st_vmw += tw1 - tw0;
+            tw0 = tw1;
+          }
           __builtin_amdgcn_s_barrier();
           asm volatile("" ::: "memory");
+          if constexpr (ST) st_wait += realtime() - tw0;
         }
         __builtin_amdgcn_sched_barrier(0);
         // fragments of it+1's first step (its images: the slot queues' second entries), then
@@ -790,7 +798,7 @@ __global__ __launch_bounds__(WNT, 1) void gemm_bf16q_kernel(PParams pp) {
     const unsigned long long st3 = realtime();
     if (threadIdx.x == 0) {
       unsigned long long* o = pp.stamps + 8 * (size_t)blockIdx.x;
-      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = st_iss;
+      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = st_iss; o[5] = st_wait; o[6] = st_vmw;
     }
   }
 }

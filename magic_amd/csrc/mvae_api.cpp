@@ -1550,7 +1550,7 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
     if (sb) (void)hipFree(sb);
     int n = 0;
     unsigned long long lo = ~0ull, hi = 0;
-    double seg[3] = {0, 0, 0}, iss = 0;
+    double seg[3] = {0, 0, 0}, iss = 0, wsum = 0, vsum = 0;
     int niss = 0;
     for (int i = 0; i < nmax && e == hipSuccess; ++i) {
       const unsigned long long* q = &h[8 * (size_t)i];
@@ -1559,8 +1559,11 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
       lo = std::min(lo, q[0]); hi = std::max(hi, q[3]);
       for (int k = 0; k < 3; ++k) seg[k] += (double)(q[k + 1] - q[k]) * 0.01;
       if (q[4]) { iss += (double)(q[4] - q[2]) * 0.01; ++niss; }
+      wsum += (double)q[5] * 0.01;
+      vsum += (double)q[6] * 0.01;
     }
     if (niss) std::fprintf(stderr, "[stamps] epilogue stores issued after %.2f us (mean of %d WGs)\n", iss / niss, niss);
+    if (n) std::fprintf(stderr, "[stamps] k-loop iteration boundaries (wave 0): vmcnt wait %.2f us, barrier %.2f us per WG\n", vsum / n, wsum / n);
     if (n) {
       std::vector<double> st0s, ends;
       for (int i = 0; i < nmax; ++i) {
