@@ -426,7 +426,7 @@ __global__ void metric_kernel(const float* __restrict__ z, int ldz, const float*
       const float rk = rsqrtf(fmaxf(colsq[L + i], L2_EPS));
       raw += (l * rl) * (k * rk);
     };
-    if ((L & 3) == 0 && L >= 256 && (ldz & 3) == 0) {  // 16-B loads, 4 elements per lane
+    if ((L & 3) == 0 && L >= 64 && (ldz & 3) == 0) {  // 16-B loads, 4 elements per lane
       for (int i = 4 * lane; i < L; i += 256) {
         const float4 l = *reinterpret_cast<const float4*>(zl + i);
         const float4 k = *reinterpret_cast<const float4*>(zk + i);
@@ -465,9 +465,19 @@ __global__ void loss_reduce_kernel(const float* __restrict__ rowvals, int B, flo
                                    float* __restrict__ losses) {
   __shared__ float red[4][256];
   float a[4] = {0.f, 0.f, 0.f, 0.f};
-  for (int b = threadIdx.x; b < B; b += 256) {
+  // rows tid, tid + 256, ... in order; 8 rows' 16-B loads issued before their sums
+  const float4* rv = reinterpret_cast<const float4*>(rowvals);
+  int b = threadIdx.x;
+  for (; b + 7 * 256 < B; b += 8 * 256) {
+    float4 t[8];
 #pragma unroll
-    for (int q = 0; q < 4; ++q) a[q] += rowvals[4 * (size_t)b + q];
+    for (int i = 0; i < 8; ++i) t[i] = rv[b + 256 * i];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { a[0] += t[i].x; a[1] += t[i].y; a[2] += t[i].z; a[3] += t[i].w; }
+  }
+  for (; b < B; b += 256) {
+    const float4 t = rv[b];
+    a[0] += t.x; a[1] += t.y; a[2] += t.z; a[3] += t.w;
   }
 #pragma unroll
   for (int q = 0; q < 4; ++q) red[q][threadIdx.x] = a[q];
