@@ -1203,6 +1203,11 @@ int gemm_bf16_wide_tn(const GemmDesc& d, size_t max_ws) { return wide_plan(d, ma
 
 int gemm_bf16_wide_tm(const GemmDesc& d, size_t max_ws) { return wide_plan(d, max_ws).tm; }
 
+void gemm_bf16_wide_plan(const GemmDesc& d, size_t max_ws, int* split, int* tn, int* tm) {
+  const WidePlan pl = wide_plan(d, max_ws);
+  *split = pl.split; *tn = pl.tn; *tm = pl.tm;
+}
+
 hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, hipStream_t st) {
   PParams p;
   p.g = g;

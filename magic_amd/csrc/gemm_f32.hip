@@ -380,10 +380,15 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   p.ntm = (d.M + BM - 1) / BM; p.ntn = (d.N + BN - 1) / BN;
   p.epi = d.epi;
   if (d.prec == GEMM_F32) p.epi.xdyn = nullptr;  // fp32 kernels read the fp32 BCE target
-  const int split = d.split > 0 ? d.split : gemm_plan_split(d, ws ? ws_elems : 0);
+  // one planner pass: split-K and (bf16 DMA kernels) the ring tile
+  const size_t wsz = ws ? ws_elems : 0;
+  int split = 1;
+  p.tn = 0;
+  p.tm = 256;
+  if (!d.valu && gemm_bf16_wide(d)) gemm_bf16_wide_plan(d, wsz, &split, &p.tn, &p.tm);
+  else split = gemm_plan_split(d, wsz);
+  if (d.split > 0) split = d.split;
   p.split = split;
-  p.tn = gemm_bf16_wide(d) ? gemm_bf16_wide_tn(d, ws ? ws_elems : 0) : 0;
-  p.tm = gemm_bf16_wide(d) ? gemm_bf16_wide_tm(d, ws ? ws_elems : 0) : 256;
   const int kb = d.prec == GEMM_F32 ? BK : 64;  // k-tile of the kernel that runs
   const int ktiles = (d.K + kb - 1) / kb;
   p.kchunk = ((ktiles + split - 1) / split) * kb;

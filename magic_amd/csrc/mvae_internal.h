@@ -103,6 +103,8 @@ int gemm_bf16_wide_split(const GemmDesc& d, size_t max_ws);
 int gemm_bf16_wide_tn(const GemmDesc& d, size_t max_ws);
 // ... and its tile M (256, or 192: k-contiguous A, not the BCE head)
 int gemm_bf16_wide_tm(const GemmDesc& d, size_t max_ws);
+// split-K, tile N and tile M of one plan (one planner pass per launch)
+void gemm_bf16_wide_plan(const GemmDesc& d, size_t max_ws, int* split, int* tn, int* tm);
 // Number of column blocks the BCE epilogue writes per row (rowpart's inner dim).
 int gemm_bce_nblk(int N);
 
