@@ -72,6 +72,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the configs block (C3 / C5 on one GPU; C4 / C5 with N ranks)")
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive h2d leg")
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="skip the input-pipeline leg (inputs() -> HIP batch producer -> step)")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launcher / data-parallel / timing / JSON path "
                          "(gloo, a stand-in engine; no GPU, no kernels, not a measurement)")
@@ -463,12 +465,17 @@ def dry_run_batch(cfg, world, rank, j):
 
 
 # ------------------------------------------------------------------------ measurement
-def measure(args, cfg, world, rank, local, dev, *, timing, steps, warmup, keep=False, h2d=False):
+def measure(args, cfg, world, rank, local, dev, *, timing, steps, warmup, keep=False, h2d=False,
+            pipeline=False):
     """One configuration through the training step: W warm-up steps, a region pass (HIP events
     around every region, outside the timed loop), K timed steps bracketed by barrier + device
     sync (max over ranks), overlap-MSE on a held-out batch. h2d: a further timed loop in which
     every step's X first comes from pinned host memory (copied on a side stream one step ahead,
-    mirroring feed_dict, 11a/vae.py:399-402). Returns a dict; the engine stays open with keep."""
+    mirroring feed_dict, 11a/vae.py:399-402). pipeline: a further timed loop fed by the input
+    pipeline itself -- inputs() over uint8 pair tables resident in HBM, each step's shuffled
+    draw and rotation angles on the host, the batch assembled by the HIP producer
+    (11a/overlap_input.py:127-261) -- and the producer kernel's own rate. Returns a dict; the
+    engine stays open with keep."""
     import torch
     import torch.distributed as dist
 
@@ -580,6 +587,36 @@ def measure(args, cfg, world, rank, local, dev, *, timing, steps, warmup, keep=F
                       "note": "PCIe-inclusive: each step's X [B, 3D] f32 copied pinned host -> HBM "
                               "(one step ahead on a copy stream), mirroring feed_dict "
                               "(11a/vae.py:399-402); never the headline value"}
+    if pipeline and not args.dry_run:
+        from magic_amd.overlap_input import BatchStream, make_batch
+        bs = BatchStream(cfg.batch, cfg.image_size, normalize=True, seed=7 + rank, device=dev)
+        for _ in range(2):
+            stepper.step(*next(bs))
+        el_p = timed(steps, lambda i: next(bs))
+        # the producer kernel alone: HIP events around back-to-back launches on one batch's draw
+        idx = torch.arange(cfg.batch, dtype=torch.int32, device=dev) % bs.locks.shape[0]
+        coef = torch.from_numpy(np.tile(np.array([[0.6, 0.8, 10.0, -20.0]], np.float32),
+                                        (cfg.batch, 1))).to(dev)
+        xb = torch.empty(cfg.batch, 3 * cfg.D, device=dev)
+        make_batch(bs.locks, bs.keys, idx, coef, out=xb)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        nk = 10
+        e0.record()
+        for _ in range(nk):
+            make_batch(bs.locks, bs.keys, idx, coef, out=xb)
+        e1.record()
+        e1.synchronize()
+        mb_ms = e0.elapsed_time(e1) / nk
+        mb_bytes = cfg.batch * cfg.D * (12 + 2)  # X written (3 fp32 / pixel) + lock and key bytes
+        out["pipeline"] = {"value": round(cfg.batch * world * steps / el_p, 2), "unit": "shape-pairs/s",
+                           "ms_per_step": round(el_p / steps * 1e3, 4),
+                           "make_batch": {"avg_ms": round(mb_ms, 4), "bytes": mb_bytes,
+                                          "gbs": round(mb_bytes / (mb_ms * 1e-3) / 1e9, 1),
+                                          "frac": round(mb_bytes / (mb_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
+                           "note": "inputs() -> partial_fit: a pool of 960 synthetic uint8 pairs in "
+                                   "HBM, per step a host shuffle draw + U[0,2pi) angles (11a/overlap_"
+                                   "input.py:127-261), rotation/interleave//255 by the HIP batch "
+                                   "producer (mvae_make_batch), then the training step"}
     # overlap-MSE on a held-out seeded batch (11a/main.py:94-111; 1/pred for reciprocal)
     if args.dry_run:
         xe, ae = dry_run_batch(cfg, world, rank, 99)
@@ -756,7 +793,7 @@ def main():
         return
 
     head = measure(args, cfg, world, rank, local, dev, timing=timing, steps=args.steps,
-                   warmup=args.warmup, keep=True, h2d=not args.no_h2d)
+                   warmup=args.warmup, keep=True, h2d=not args.no_h2d, pipeline=not args.no_pipeline)
     eng = head.pop("eng")
     if rank == 0:
         print_regions(args, head, f"{args.config}")
@@ -771,7 +808,7 @@ def main():
                 continue
             c = config_of("C3" if cid == "C4" else cid, small=args.dry_run)
             m = measure(args, c, world, rank, local, dev, timing=timing, steps=args.steps,
-                        warmup=args.warmup)
+                        warmup=args.warmup, pipeline=not args.no_pipeline)
             if rank == 0:
                 print_regions(args, m, cid)
                 rf, lr = rooflines(args, m)
@@ -782,7 +819,7 @@ def main():
                               "ms_per_step": round(m["elapsed"] / m["steps"] * 1e3, 4),
                               "global_batch": c.batch * world, "per_gpu_batch": c.batch,
                               "dtype": c.precision, "overlap_mse": round(m["mse"], 2),
-                              "roofline": rf, "loss_roofline": lr}
+                              "roofline": rf, "loss_roofline": lr, "pipeline": m.get("pipeline")}
 
     if rank == 0:
         pairs = cfg.batch * world * args.steps
@@ -835,6 +872,7 @@ def main():
             "loss_roofline": loss_roofline,
             "cpu_baseline": cpu,
             "h2d": head.get("h2d"),
+            "pipeline": head.get("pipeline"),
             "configs": extra,
             "build_id": None if args.dry_run else _lib.load().mvae_build_id().decode(),
         }

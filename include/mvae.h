@@ -102,7 +102,12 @@ enum {
   MVAE_BUF_DIST = 6,     /* float[B]: distance of the last forward                      */
   MVAE_BUF_GRADS_DEC = 7,/* decoder slice of g1 (ready first in mvae_backward)         */
   MVAE_BUF_DEAD = 8,     /* the never-trained decoder log-sigma variables               */
-  MVAE_BUF_EPS = 9,      /* float[3,B,L]: eps of the last forward (given or generated)  */
+  MVAE_BUF_EPS = 9,      /* float[3,B,L]: eps of the last forward (given or generated).  */
+                         /* A generated draw is regenerated inside the latent kernels and */
+                         /* written to this buffer only when it is requested: the call    */
+                         /* synchronises the device (hipDeviceSynchronize) and the pointer */
+                         /* holds the draw of the forward BEFORE the call -- re-fetch it  */
+                         /* after every forward whose eps you read.                        */
   MVAE_BUF_DYN = 10      /* int32[1] (count 1): nonzero when the last batch's pixels are
                             not all exact in bf16 (f32x: the layer-0 GEMMs then run all 6
                             plane pairs instead of 3; bf16/f32x: the BCE target is read in

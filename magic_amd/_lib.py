@@ -141,7 +141,12 @@ def verify_build(lib, expected: str | None = None) -> str:
     is refused. Returns the id."""
     from .build import source_hash
     got = lib.mvae_build_id().decode()
-    want = expected if expected is not None else source_hash()
+    try:
+        want = expected if expected is not None else source_hash()
+    except FileNotFoundError as e:
+        raise MVAELibraryError(
+            f"cannot verify libmvae.so (build id {got}): source file missing ({e.filename}); the "
+            "library is only loaded from a tree holding the sources it was built from") from e
     if got != want:
         raise MVAELibraryError(
             f"libmvae.so build id {got} does not match the sources on disk ({want}): the library "

@@ -8,7 +8,6 @@ The library carries ``source_hash()`` of the sources it was built from (``mvae_b
 from __future__ import annotations
 
 import concurrent.futures as cf
-import glob
 import hashlib
 import os
 import subprocess
@@ -21,7 +20,7 @@ OBJ = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libmvae.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MVAE_ARCH", "gfx950")
-SOURCES = ["mvae_api.cpp", "gemm_f32.hip", "gemm_bf16.hip", "gemm_valu.hip", "mvae_kernels.hip",
+SOURCES = ["mvae_api.cpp", "gemm_f32.hip", "gemm_bf16.hip", "gemm_bf16e.hip", "gemm_valu.hip", "mvae_kernels.hip",
            "conv_tower.hip", "conv_mfma.hip"]
 HEADERS = ["mvae_internal.h", "gemm_common.h", os.path.join("..", "..", "include", "mvae.h")]
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result",
@@ -29,13 +28,14 @@ CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-r
 
 
 def source_files() -> list[str]:
-    """Every file the library is built from: magic_amd/csrc/* and include/mvae.h."""
-    fs = sorted(p for p in glob.glob(os.path.join(CSRC, "*")) if os.path.isfile(p))
-    return fs + [os.path.join(ROOT, "include", "mvae.h")]
+    """The files the library is compiled from: SOURCES and HEADERS (include/mvae.h among them).
+    Nothing else under csrc/ (editor files, -save-temps output) enters the build id."""
+    return sorted(os.path.normpath(os.path.join(CSRC, f)) for f in SOURCES + HEADERS)
 
 
 def source_hash() -> str:
-    """First 16 hex digits of SHA-256 over (relative path, NUL, contents) of source_files()."""
+    """First 16 hex digits of SHA-256 over (relative path, NUL, contents) of source_files().
+    Raises FileNotFoundError naming the missing file when a source is absent."""
     h = hashlib.sha256()
     for p in source_files():
         h.update(os.path.relpath(p, ROOT).replace(os.sep, "/").encode() + b"\0")

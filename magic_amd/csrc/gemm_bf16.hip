@@ -42,20 +42,6 @@ struct Geo {
   static constexpr int NLD = 128 * BK / 8 / NT;                         // 16-B loads / thread
 };
 
-struct PParams {
-  Params g;                         // shapes, fp32 output, batch/split/tiles, epilogue
-  const unsigned short* A; long long pA;
-  const unsigned short* B; long long pB;
-  int npairs, npairs0;
-  unsigned char pa[6], pb[6];
-  int pab;                          // pa[i] | pb[i] << 2 packed 4 bits per pair (no memory reads)
-  const int* dyn;                   // A residual planes nonzero? (nullptr: use all pairs)
-  int diag;                         // timing diagnostics: bit 0 = no operand copies after the
-                                    // prologue (the k-loop multiplies stale LDS images)
-  unsigned long long* stamps;       // stamped diagnostics builds (ST): 8 slots per workgroup
-                                    // {start, prologue landed, k-loop done, end, stores issued}
-};
-
 // 100 MHz constant-rate stamp, workgroup-comparable (diagnostics builds only)
 __device__ __forceinline__ unsigned long long realtime() {
   unsigned long long t;
@@ -209,11 +195,10 @@ __global__ __launch_bounds__(NT, 2) void gemm_bf16p_kernel(PParams pp) {
 }
 
 // ---------------------------------------------------------------------------------------
-// Wide kernel: 256x256x64 tile, 512 threads = 8 waves (2 along M x 4 along N), each wave
+// Wide kernels: 256x256x64 tile, 512 threads = 8 waves (2 along M x 4 along N), each wave
 // 128x64 = 4x2 MFMA 32x32x16 accumulators (1024 MFMA cycles per k-tile per wave). Operand
-// tiles are copied HBM -> LDS by global_load_lds_dwordx4 (no VGPR staging): two LDS stages
-// of 2 x 32 KB, the next k-tile's copy in flight during the MFMAs of the current one, one
-// barrier per k-tile. The LDS images are lane-linear (the DMA's destination is wave base +
+// tiles are copied HBM -> LDS by global_load_lds_dwordx4 (no VGPR staging). The LDS images
+// are lane-linear (the DMA's destination is wave base +
 // 16 B x lane); bank-conflict-free fragment reads come from XOR swizzles applied to the
 // per-lane SOURCE address and undone on the read:
 //   k-contiguous operand: image [256 rows][8 chunks of 8 k], chunk c of row r at position
@@ -315,20 +300,6 @@ __device__ __forceinline__ void wait_lds() {
   else if constexpr (N == 12) asm volatile("s_waitcnt lgkmcnt(12)" ::: "memory");
   else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 }
-// wait until at most n (runtime: 0, g or 2g for g DMA instructions per tile) are outstanding
-template <int G>
-__device__ __forceinline__ void wait_dma(int tiles) {
-  if (tiles <= 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else if (tiles == 1) {
-    if constexpr (G == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-  } else {
-    if constexpr (G == 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-  }
-}
-
 // wait until at most N vector-memory operations are outstanding (N literal per instantiation)
 template <int N>
 __device__ __forceinline__ void wait_vm() {
@@ -338,229 +309,12 @@ __device__ __forceinline__ void wait_vm() {
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// BK: k-tile depth; DEPTH LDS stages, the copy of tile it + DEPTH - 1 issued while tile it is
-// multiplied. DEPTH 2 waits for the next tile's copy at every barrier (vmcnt(0)); deeper
-// pipelines keep DEPTH - 2 copies in flight across the barrier, which therefore is a raw
-// s_barrier (__syncthreads() would wait for every outstanding LDS-DMA).
-template <bool AT, bool BT, int EPI, int BK, int DEPTH>
-__global__ __launch_bounds__(WNT, 1) void gemm_bf16w_kernel(PParams pp) {
-  constexpr int IMG = WT * BK;  // bf16 elements per operand image
-  const Params& p = pp.g;
-  if (epi_skip<EPI>(p.epi)) return;
-  __shared__ __attribute__((aligned(16))) short smem[DEPTH * 2 * IMG];  // [stage][A | B]
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const Tile t = tile_of_t<WT, WT>(p, true);
-  const unsigned short* __restrict__ A = pp.A + t.bi * p.sA;
-  const unsigned short* __restrict__ Bm = pp.B + t.bi * p.sB;
-
-  WLoad<!AT, BK> la;
-  WLoad<BT, BK> lb;
-  la.init(p.lda, t.m0, p.M, wave, lane);
-  lb.init(p.ldb, t.n0, p.N, wave, lane);
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int npairs = (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
-  const int nkt = t.ks < t.ke ? (t.ke - t.ks + BK - 1) / BK : 0;
-  const int total = npairs * nkt;
-  int ipr = 0, ikt = 0;  // (pair, k-tile) of the next copy
-  auto issue = [&](int stage) {
-    short* img = smem + stage * 2 * IMG;
-    const int k0 = t.ks + ikt * BK;
-    const int pab = pp.pab >> (4 * ipr);
-    la.issue(A + (pab & 3) * pp.pA, p.lda, k0, t.ke, img, wave);
-    lb.issue(Bm + ((pab >> 2) & 3) * pp.pB, p.ldb, k0, t.ke, img + IMG, wave);
-    if (++ikt == nkt) { ikt = 0; ++ipr; }
-  };
-  constexpr int NRD = 4 * WLoad<!AT, BK>::NRD + 2 * WLoad<BT, BK>::NRD;  // LDS reads / k16-step
-  constexpr int G = 2 * (BK / 16);  // DMA instructions per thread per tile
-  const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
-#pragma unroll
-  for (int s = 0; s < DEPTH - 1; ++s)
-    if (s < total) issue(s);
-  for (int it = 0; it < total; ++it) {
-    const int stage = it % DEPTH;
-    if constexpr (DEPTH == 2) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();  // tile it landed for all waves; the other stage is no longer read
-    } else {
-      const int issued = min(total, it + DEPTH - 1);
-      wait_dma<G>(issued - it - 1);  // this wave's copies of tile it have landed
-      __builtin_amdgcn_s_barrier();  // ... for every wave; stage (it-1) % DEPTH no longer read
-      asm volatile("" ::: "memory");
-    }
-    if (it + DEPTH - 1 < total) issue((it + DEPTH - 1) % DEPTH);
-    const short* sa = smem + stage * 2 * IMG;
-    const short* sb = sa + IMG;
-    const unsigned la0 = lds0 + 2u * (unsigned)(stage * 2 * IMG);
-    const unsigned lb0 = la0 + 2u * IMG;
-    bf16x8 fa[2][4], fb[2][2];
-    auto rd = [&](int ks, bf16x8 (&a)[4], bf16x8 (&b)[2]) {
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni) b[ni] = lb.frag(sb, lb0, wn * 64 + ni * 32, ks, lane);
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) a[mi] = la.frag(sa, la0, wm * 128 + mi * 32, ks, lane);
-    };
-    rd(0, fa[0], fb[0]);
-#pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      if (ks + 1 < BK / 16) {
-        rd(ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
-        wait_lds<NRD>();
-      } else {
-        wait_lds<0>();
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks & 1][mi], fb[ks & 1][ni],
-                                                                acc[mi][ni], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  // C/D-layout epilogue: one 128-B row segment per half-wave store. (An LDS-transposed form
-  // with 16-B row stores measured slower on every step shape and spills with BCE.)
-  epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
-}
-
 // ---------------------------------------------------------------------------------------
-// Ring form of the wide kernel (same 256x256x64 tile, waves, fragments and epilogue). The
-// k-loop walks (k-tile, plane pair) with the pairs INNERMOST, and the A and B operand images
-// live in LDS rings of 3 and 2 slots (5 x 32 KB = the CU's 160 KB): an image is copied only
-// when the iteration's (plane, k-tile) differs from the previous iteration's. The split's
-// pairs are ordered (0,0) (0,1) (0,2) (1,0) (1,1) (2,0), so with binary pixels (pairs with
-// i = 0 only) the layer-0 operand is copied once per k-tile instead of once per pair, and with
-// six pairs A is copied 3 and B 6 times per k-tile instead of 6 + 6.
-// Pipeline: iteration it opens with a counted vmcnt (its B image, issued in it-1, and its A
-// image, issued in it-2, have landed; the A copy for it+1 stays in flight across the barrier)
-// and a raw s_barrier; it then issues the B copy for it+1 and, after its first k16-step, the
-// A copy for it+2, each into a ring slot whose last reader finished before the barrier.
-// SP: s_setprio 1 around each MFMA cluster (cdna_hip_programming.md T5).
-template <bool AT, bool BT, int EPI, bool SP>
-__global__ __launch_bounds__(WNT, 1) void gemm_bf16r_kernel(PParams pp) {
-  constexpr int BK = 64;
-  constexpr int IMG = WT * BK;  // bf16 elements per operand image
-  const Params& p = pp.g;
-  if (epi_skip<EPI>(p.epi)) return;
-  __shared__ __attribute__((aligned(16))) short smem[5 * IMG];  // A slots 0-2 | B slots 0-1
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  const Tile t = tile_of_t<WT, WT>(p, true);
-  const unsigned short* __restrict__ A = pp.A + t.bi * p.sA;
-  const unsigned short* __restrict__ Bm = pp.B + t.bi * p.sB;
-
-  WLoad<!AT, BK> la;
-  WLoad<BT, BK> lb;
-  la.init(p.lda, t.m0, p.M, wave, lane);
-  lb.init(p.ldb, t.n0, p.N, wave, lane);
-
-  f32x16 acc[4][2];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int np = (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
-  const int nkt = t.ks < t.ke ? (t.ke - t.ks + BK - 1) / BK : 0;
-  const int total = np * nkt;
-  constexpr int NRD = 4 * WLoad<!AT, BK>::NRD + 2 * WLoad<BT, BK>::NRD;  // LDS reads / k16-step
-  const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
-
-  // cursors: (k-tile, pair) of iterations it (cur), it+1 (n1) and it+2 (n2)
-  auto adv = [&](int& kt, int& pr) { if (++pr == np) { pr = 0; ++kt; } };
-  auto pa_of = [&](int pr) { return (pp.pab >> (4 * pr)) & 3; };
-  auto pb_of = [&](int pr) { return (pp.pab >> (4 * pr + 2)) & 3; };
-  int kt0 = 0, pr0 = 0, kt1 = 0, pr1 = 0, kt2 = 0, pr2 = 0;
-  adv(kt1, pr1);
-  adv(kt2, pr2); adv(kt2, pr2);
-  // ring slots of the images of it, it+1, it+2 (A) and it, it+1 (B)
-  int sa0 = 0, sa1 = 0, sa2 = 0, sb0 = 0;
-  bool na1 = false;  // A image of it+1 is a new copy (issued, possibly still in flight)
-  if (total > 0) {
-    la.issue(A + pa_of(0) * pp.pA, p.lda, t.ks, t.ke, smem, wave);
-    lb.issue(Bm + pb_of(0) * pp.pB, p.ldb, t.ks, t.ke, smem + 3 * IMG, wave);
-    if (total > 1) {
-      na1 = kt1 != kt0 || pa_of(pr1) != pa_of(pr0);
-      sa1 = na1 ? 1 : 0;
-      if (na1) la.issue(A + pa_of(pr1) * pp.pA, p.lda, t.ks + kt1 * BK, t.ke, smem + IMG, wave);
-    }
-  }
-  for (int it = 0; it < total; ++it) {
-    // images of it landed (this wave's copies), then for every wave
-    if (na1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    // B copy for it+1 (needed first), A copy for it+2 (after the first k16-step)
-    const bool dma = !(pp.diag & 1);
-    const bool nb1 = dma && it + 1 < total && (kt1 != kt0 || pb_of(pr1) != pb_of(pr0));
-    const int sb1 = nb1 ? sb0 ^ 1 : sb0;
-    if (nb1) lb.issue(Bm + pb_of(pr1) * pp.pB, p.ldb, t.ks + kt1 * BK, t.ke,
-                      smem + (3 + sb1) * IMG, wave);
-    const bool na2 = dma && it + 2 < total && (kt2 != kt1 || pa_of(pr2) != pa_of(pr1));
-    sa2 = na2 ? (sa1 == 2 ? 0 : sa1 + 1) : sa1;
-    const short* sa = smem + sa0 * IMG;
-    const short* sb = smem + (3 + sb0) * IMG;
-    const unsigned la0 = lds0 + 2u * (unsigned)(sa0 * IMG);
-    const unsigned lb0 = lds0 + 2u * (unsigned)((3 + sb0) * IMG);
-    bf16x8 fa[2][4], fb[2][2];
-    auto rd = [&](int ks, bf16x8 (&a)[4], bf16x8 (&b)[2]) {
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni) b[ni] = lb.frag(sb, lb0, wn * 64 + ni * 32, ks, lane);
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) a[mi] = la.frag(sa, la0, wm * 128 + mi * 32, ks, lane);
-    };
-    rd(0, fa[0], fb[0]);
-#pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      if (ks + 1 < BK / 16) {
-        rd(ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
-        wait_lds<NRD>();
-      } else {
-        wait_lds<0>();
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (SP) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks & 1][mi], fb[ks & 1][ni],
-                                                                acc[mi][ni], 0, 0, 0);
-      if constexpr (SP) __builtin_amdgcn_s_setprio(0);
-      __builtin_amdgcn_sched_barrier(0);
-      if (ks == 0 && na2)
-        la.issue(A + pa_of(pr2) * pp.pA, p.lda, t.ks + kt2 * BK, t.ke, smem + sa2 * IMG, wave);
-    }
-    // shift the cursors
-    sa0 = sa1; sa1 = sa2; sb0 = sb1; na1 = na2;
-    kt0 = kt1; pr0 = pr1; kt1 = kt2; pr1 = pr2; adv(kt2, pr2);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  epilogue_g<EPI, 4, 2, WT, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
-}
-
-// ---------------------------------------------------------------------------------------
-// Interleaved ring kernel (the default wide kernel): the operand rings of gemm_bf16r_kernel,
-// with the LDS fragment reads of the NEXT k16-step issued between the MFMAs of the current one
+// Interleaved ring kernel: the k-loop walks (k-tile, plane pair) with the pairs INNERMOST, and
+// the A and B operand images live in LDS rings of 3 and 2 slots (5 x 32 KB = the CU's 160 KB):
+// an image is copied only when the iteration's (plane, k-tile) differs from the previous
+// iteration's (with binary pixels the layer-0 operand is copied once per k-tile for its three
+// pairs). The LDS fragment reads of the NEXT k16-step issued between the MFMAs of the current one
 // (one fragment per MFMA gap; MI355X_MICROARCH.md §LDS: up to three reads per 32x32x16 gap are
 // free), so no k16-step waits for its reads and no read burst stalls the MFMA issue. The
 // iteration hand-off sits inside the last k16-step: once the step's fragments are in registers
@@ -837,210 +591,6 @@ hipError_t launch_q_t(const PParams& p, bool at, bool bt, hipStream_t st) {
   return p.g.tn == 128 ? launch_q_l<EPI, TE, 128>(p, at, bt, st) : launch_q_l<EPI, TE, 256>(p, at, bt, st);
 }
 
-// ---------------------------------------------------------------------------------------
-// Twin kernel: 128x128x64 tile, 256 threads = 4 waves (2x2), each wave 64x64 = 2x2 MFMA
-// 32x32x16 accumulators; operand images HBM -> LDS by global_load_lds_dwordx4 (the wide
-// kernels' swizzled lane-linear images at 128 rows) into two stages of 2 x 16 KB. 64 KB of LDS
-// and <= 256 VGPRs, so TWO workgroups share a CU: one's epilogue (activation / BCE math, the
-// LDS transpose and 16-B row stores of the fp32 output and bf16 planes) and its prologue DMA
-// latency run beside the other's k-loop. For the GEMMs whose K is short or whose N ~ 500
-// (hidden encoder layers, the 500-wide dgrads, the BCE decoder output): on the one-workgroup
-// 256-row kernels each tile's epilogue and prologue are exposed, and 500-wide outputs give too
-// few 256x256 tiles to fill 256 CUs without split-K slabs.
-// Pipeline: one barrier per k-tile; the copy of iteration it+1 is issued right after it, into
-// the stage iteration it-1 read, and waited for (vmcnt(0)) at the top of it+1.
-constexpr int TT = 128, TNT = 256;
-
-// BK x DEPTH: 64 x 2 stages (one k-tile in flight, vmcnt(0) at each barrier) or 32 x 4 (three
-// in flight behind a counted vmcnt and a raw barrier), both 64 KB of LDS.
-template <bool AT, bool BT, int EPI, bool TE, bool ST = false, int BK = 64, int DEPTH = 2>
-__global__ __launch_bounds__(TNT, 2) void gemm_bf16t_kernel(PParams pp) {
-  constexpr int IMG = TT * BK;  // bf16 elements per operand image
-  const Params& p = pp.g;
-  if (epi_skip<EPI>(p.epi)) return;
-  unsigned long long st0 = 0, st1 = 0, st2 = 0;
-  if constexpr (ST) {
-    __builtin_amdgcn_sched_barrier(0);
-    st0 = realtime();
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  __shared__ __attribute__((aligned(16))) short smem[DEPTH * 2 * IMG];  // [stage][A | B] = 64 KB
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  const Tile t = tile_of_t<TT, TT>(p, true);
-  const unsigned short* __restrict__ A = pp.A + t.bi * p.sA;
-  const unsigned short* __restrict__ Bm = pp.B + t.bi * p.sB;
-
-  WLoad<!AT, BK, TT, 4> la;
-  WLoad<BT, BK, TT, 4> lb;
-  la.init(p.lda, t.m0, p.M, wave, lane);
-  lb.init(p.ldb, t.n0, p.N, wave, lane);
-
-  f32x16 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int np = (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
-  const int nkt = t.ks < t.ke ? (t.ke - t.ks + BK - 1) / BK : 0;
-  const int total = np * nkt;
-  int ipr = 0, ikt = 0;  // (pair, k-tile) of the next copy
-  auto issue = [&](int stage) {
-    short* img = smem + stage * 2 * IMG;
-    const int k0 = t.ks + ikt * BK;
-    const int pab = pp.pab >> (4 * ipr);
-    la.issue(A + (pab & 3) * pp.pA, p.lda, k0, t.ke, img, wave);
-    lb.issue(Bm + ((pab >> 2) & 3) * pp.pB, p.ldb, k0, t.ke, img + IMG, wave);
-    if (++ikt == nkt) { ikt = 0; ++ipr; }
-  };
-  constexpr int NRD = 2 * WLoad<!AT, BK, TT, 4>::NRD + 2 * WLoad<BT, BK, TT, 4>::NRD;
-  constexpr int G = WLoad<!AT, BK, TT, 4>::NG + WLoad<BT, BK, TT, 4>::NG;  // DMA instrs per tile
-  const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
-#pragma unroll
-  for (int s = 0; s < DEPTH - 1; ++s)
-    if (s < total) issue(s);
-  for (int it = 0; it < total; ++it) {
-    const int stage = it % DEPTH;
-    if constexpr (DEPTH == 2) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else {
-      const int issued = min(total, it + DEPTH - 1);
-      wait_dma<G>(issued - it - 1);  // this wave's copies of tile it have landed
-    }
-    __builtin_amdgcn_s_barrier();  // tile it landed for every wave; stage it-1 no longer read
-    asm volatile("" ::: "memory");
-    if constexpr (ST) {
-      if (it == 0) {
-        __builtin_amdgcn_sched_barrier(0);
-        st1 = realtime();
-        __builtin_amdgcn_sched_barrier(0);
-      }
-    }
-    if (it + DEPTH - 1 < total && !(pp.diag & 1)) issue((it + DEPTH - 1) % DEPTH);
-    const short* sa = smem + stage * 2 * IMG;
-    const short* sb = sa + IMG;
-    const unsigned la0 = lds0 + 2u * (unsigned)(stage * 2 * IMG);
-    const unsigned lb0 = la0 + 2u * IMG;
-    bf16x8 fa[2][2], fb[2][2];
-    auto rd = [&](int ks, bf16x8 (&a)[2], bf16x8 (&b)[2]) {
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni) b[ni] = lb.frag(sb, lb0, wn * 64 + ni * 32, ks, lane);
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi) a[mi] = la.frag(sa, la0, wm * 64 + mi * 32, ks, lane);
-    };
-    rd(0, fa[0], fb[0]);
-#pragma unroll
-    for (int ks = 0; ks < BK / 16; ++ks) {
-      if (ks + 1 < BK / 16) {
-        rd(ks + 1, fa[(ks + 1) & 1], fb[(ks + 1) & 1]);
-        wait_lds<NRD>();
-      } else {
-        wait_lds<0>();
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni)
-          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks & 1][mi], fb[ks & 1][ni],
-                                                                acc[mi][ni], 0, 0, 0);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if constexpr (ST) {
-    __builtin_amdgcn_sched_barrier(0);
-    st2 = realtime();
-    __builtin_amdgcn_sched_barrier(0);
-  }
-  unsigned long long st_iss = 0;
-  if constexpr (TE) epilogue_rm<EPI, 2, 2, 2, TNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag,
-                                                    ST ? &st_iss : nullptr);
-  else epilogue_g<EPI, 2, 2, TT, 2>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
-  if constexpr (ST) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const unsigned long long st3 = realtime();
-    if (threadIdx.x == 0) {
-      unsigned long long* o = pp.stamps + 8 * (size_t)blockIdx.x;
-      o[0] = st0; o[1] = st1; o[2] = st2; o[3] = st3; o[4] = st_iss;
-    }
-  }
-}
-
-// MVAE_TWIN_BK (diagnostics A/B): 32 = the 4-stage BK-32 pipeline, else 64 x 2 stages
-static int twin_bk() {
-  static const int bk = [] {
-    const char* v = std::getenv("MVAE_TWIN_BK");
-    return v && std::atoi(v) == 32 ? 32 : 64;
-  }();
-  return bk;
-}
-
-template <bool AT, bool BT, int EPI, bool TE>
-hipError_t launch_tw(const PParams& p, hipStream_t st) {
-  const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
-  const bool deep = twin_bk() == 32;
-  if constexpr (EPI == EPI_ACT && TE) {  // the stamped diagnostics build (mvae_bench_gemm only)
-    if (p.stamps) {
-      if (deep)
-        hipLaunchKernelGGL((gemm_bf16t_kernel<AT, BT, EPI, TE, true, 32, 4>), dim3(nwg), dim3(TNT), 0, st, p);
-      else
-        hipLaunchKernelGGL((gemm_bf16t_kernel<AT, BT, EPI, TE, true>), dim3(nwg), dim3(TNT), 0, st, p);
-      return hipGetLastError();
-    }
-  }
-  if (deep)
-    hipLaunchKernelGGL((gemm_bf16t_kernel<AT, BT, EPI, TE, false, 32, 4>), dim3(nwg), dim3(TNT), 0, st, p);
-  else
-    hipLaunchKernelGGL((gemm_bf16t_kernel<AT, BT, EPI, TE>), dim3(nwg), dim3(TNT), 0, st, p);
-  return hipGetLastError();
-}
-
-template <int EPI, bool TE>
-hipError_t launch_twin_l(const PParams& p, bool at, bool bt, hipStream_t st) {
-  if (!at && !bt) return launch_tw<false, false, EPI, TE>(p, st);
-  if (at && !bt) return launch_tw<true, false, EPI, TE>(p, st);
-  if (!at && bt) return launch_tw<false, true, EPI, TE>(p, st);
-  return launch_tw<true, true, EPI, TE>(p, st);
-}
-
-template <bool AT, bool BT, int EPI, bool SP>
-hipError_t launch_r(const PParams& p, hipStream_t st) {
-  const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
-  hipLaunchKernelGGL((gemm_bf16r_kernel<AT, BT, EPI, SP>), dim3(nwg), dim3(WNT), 0, st, p);
-  return hipGetLastError();
-}
-
-template <int EPI, bool SP>
-hipError_t launch_ring_t(const PParams& p, bool at, bool bt, hipStream_t st) {
-  if (!at && !bt) return launch_r<false, false, EPI, SP>(p, st);
-  if (at && !bt) return launch_r<true, false, EPI, SP>(p, st);
-  if (!at && bt) return launch_r<false, true, EPI, SP>(p, st);
-  return launch_r<true, true, EPI, SP>(p, st);
-}
-
-template <bool AT, bool BT, int EPI, int BK, int DEPTH>
-hipError_t launch_w(const PParams& p, hipStream_t st) {
-  const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
-  hipLaunchKernelGGL((gemm_bf16w_kernel<AT, BT, EPI, BK, DEPTH>), dim3(nwg), dim3(WNT), 0, st, p);
-  return hipGetLastError();
-}
-
-template <int EPI, int BK, int DEPTH>
-hipError_t launch_wide_t(const PParams& p, bool at, bool bt, hipStream_t st) {
-  if (!at && !bt) return launch_w<false, false, EPI, BK, DEPTH>(p, st);
-  if (at && !bt) return launch_w<true, false, EPI, BK, DEPTH>(p, st);
-  if (!at && bt) return launch_w<false, true, EPI, BK, DEPTH>(p, st);
-  return launch_w<true, true, EPI, BK, DEPTH>(p, st);
-}
-
 // the row-major 16-B epilogue (epilogue_wide) applies: bases and strides keep every 8-column
 // chunk of every operand it touches 16-B aligned
 bool wide_epi_vec_ok(const Params& g) {
@@ -1058,30 +608,20 @@ bool wide_epi_vec_ok(const Params& g) {
   return true;
 }
 
-// wide variants (diagnostics, EPI_STORE): 5 = two-stage form at BK 32 x 4 stages, 7 = ring form
-// with s_setprio, 8 = two-stage form at BK 64 x 2 stages; 6 = ring form (any epilogue);
-// otherwise (0, 3) the interleaved ring form
+// The planned 256-row kernel: the eight-phase kernel (tile N = TN_E8, gemm_bf16e.hip) or the
+// interleaved ring kernel. Their epilogue goes through LDS (row-major 16-B stores) when the tile
+// writes bf16 planes or is the BCE head (2-B plane stores and 4-B target loads per element
+// otherwise), and stays in the C/D layout for fp32-only outputs (split-K slabs: 128-B row
+// segments already, where the LDS round trip measured 5-10 % slower); variant 14 routes
+// fp32-only outputs of the eight-phase kernel through LDS too, variant 10 keeps the ring kernel
+// on the C/D layout.
 template <int EPI>
 hipError_t launch_wide(const PParams& p, bool at, bool bt, int variant, hipStream_t st) {
   constexpr bool BCE = EPI == EPI_BCE || EPI == EPI_BCEB;
-  if (p.g.tn == TN_TWIN) {
-    // row-major epilogue through LDS where the tile writes bf16 planes or is the BCE head
-    // (variant 14: also for fp32-only outputs)
+  if (p.g.tn == TN_E8) {
     const bool te = (p.g.epi.cp || BCE || variant == 14) && wide_epi_vec_ok(p.g);
-    return te ? launch_twin_l<EPI, true>(p, at, bt, st) : launch_twin_l<EPI, false>(p, at, bt, st);
+    return gemm_bf16e_launch(p, at, bt, EPI, te, st);
   }
-  if constexpr (EPI == EPI_STORE) {
-    if (variant == 5) return launch_wide_t<EPI, 32, 4>(p, at, bt, st);
-    if (variant == 7) return launch_ring_t<EPI, true>(p, at, bt, st);
-    if (variant == 8) return launch_wide_t<EPI, 64, 2>(p, at, bt, st);
-  }
-  // 6: the ring form of round 1 (profiles/r1/gemm_ab_ring.txt: +3..28 % over the two-stage
-  // form on the step's shapes; s_setprio around the MFMA clusters measured neutral)
-  if (variant == 6) return launch_ring_t<EPI, false>(p, at, bt, st);
-  // default: the interleaved ring form; its epilogue goes through LDS (row-major 16-B stores)
-  // when the tile writes bf16 planes or is the BCE head (2-B plane stores and 4-B target loads
-  // per element otherwise), and stays in the C/D layout for fp32-only outputs (split-K slabs:
-  // 128-B row segments already, where the LDS round trip measured 5-10 % slower)
   if ((p.g.epi.cp || BCE) && variant != 10 && wide_epi_vec_ok(p.g))
     return launch_q_t<EPI, true>(p, at, bt, st);
   return launch_q_t<EPI, false>(p, at, bt, st);
@@ -1119,11 +659,11 @@ hipError_t launch_var(const PParams& p, bool at, bool bt, int variant, hipStream
 
 bool gemm_bf16_wide(const GemmDesc& d) {
   if (d.prec == GEMM_F32) return false;
-  // 10-12, 15: default-shape variants of the interleaved kernel (old epilogue, forced tile N,
-  // no twin); 13 / 14: the twin kernel (any shape)
+  // 10-12, 15: default-shape variants of the ring kernel (C/D epilogue, forced tile N, no
+  // eight-phase kernel); 3: the ring kernel, 13 / 14: the eight-phase kernel, on any shape
   const int v = (d.variant >= 10 && d.variant != 13 && d.variant != 14) ? 0 : d.variant;
   if (v == 1 || v == 2 || v == 4) return false;  // 128x128 register-staged variants
-  if (v != 3 && v < 5 && (d.M < 256 || d.N < 256)) return false;
+  if (v != 3 && v != 13 && v != 14 && (d.M < 256 || d.N < 256)) return false;
   // one k-tile and under a CU's worth of 256x256 tiles (dec layer 1: K = L + 1; the head's
   // dgrad: K = 2L): epilogue-bound on few CUs, the 128x128 kernels spread it wider
   const long long t256 = (long long)((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
@@ -1135,11 +675,11 @@ bool gemm_bf16_wide(const GemmDesc& d) {
   return true;
 }
 
-// Joint choice of the kernel (256 x 256 / 256 x 128 one-workgroup-per-CU ring kernels, or the
-// 128 x 128 twin kernel at two workgroups per CU) and split-K: each kernel's time is its rounds
-// of resident workgroups x (k-tiles + fixed prologue/epilogue cost) x its time per k-tile;
-// split-K adds the fp32 slab round trip and the reduction launch. Variants 11 / 12 force the
-// ring kernel at tile N 128 / 256, 13 / 14 the twin kernel, 15 the ring kernels only.
+// Joint choice of the kernel (256 x 256 eight-phase kernel; 256 x 256 / 256 x 128 / 192 x 256 /
+// 192 x 128 ring kernels) and split-K: each kernel's time is its rounds of resident workgroups
+// (one per CU) x (k-tiles + fixed prologue/epilogue cost) x its time per k-tile; split-K adds the
+// fp32 slab round trip and the reduction launch. Variants 11 / 12 force the ring kernel at tile
+// N 128 / 256, 13 / 14 the eight-phase kernel, 15 the ring kernels only.
 struct WidePlan { int split = 1; int tn = 256; int tm = 256; };
 // MVAE_TM192=0 (A/B): plan the ring kernels at 256-row tiles only
 static bool tm192_enabled() {
@@ -1158,40 +698,39 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
     for (int j = 0; j < d.nB; ++j) np += i + j < T;
   if (d.dynA) np = (np + (d.nB < T ? d.nB : T)) / 2;  // A's residual planes often all zero
   const bool big = d.M >= 256 && d.N >= 256;
+  const bool force_e8 = d.variant == 13 || d.variant == 14;
+  const bool allow_e8 = force_e8 || (d.variant == 0 && big);
   double best = 1e30;
   WidePlan pl;
   // 192-row ring tiles: k-contiguous A, epilogues other than the BCE head / sigmoid
   const bool t192 = tm192_enabled() && !d.at && d.epi.mode != EPI_BCE && d.epi.mode != EPI_BCEB &&
                     d.epi.mode != EPI_SIGMOID;
   for (int cand = 0; cand < 5; ++cand) {
-    // candidates: ring 256x256, 256x128, twin 128x128, ring 192x256, 192x128
-    const int w = cand == 0 || cand == 3 ? 256 : cand == 1 || cand == 4 ? 128 : TN_TWIN;
+    // candidates: ring 256x256, 256x128, eight-phase 256x256, ring 192x256, 192x128
+    const bool e8 = cand == 2;
+    const int w = cand == 0 || cand == 3 ? 256 : cand == 1 || cand == 4 ? 128 : TN_E8;
     const int tmr = cand >= 3 ? 192 : 256;
-    const bool twin = w == TN_TWIN;
+    if (e8 ? !allow_e8 : force_e8) continue;
     if (cand >= 3 && !t192) continue;
     if ((d.tm == 192 && t192 && cand != 3 && cand != 4) || (d.tm == 256 && cand >= 3)) continue;
     if (d.variant == 11 && w != 128) continue;
     if (d.variant == 12 && w != 256) continue;
-    if ((d.variant == 13 || d.variant == 14) && !twin) continue;
-    if (d.variant == 15 && twin) continue;
-    if (!twin && !big && d.variant != 3 && d.variant < 5) continue;
-    const int tm = twin ? TT : tmr, tnn = twin ? TT : w;
-    const long long tiles = (long long)((d.M + tm - 1) / tm) * ((d.N + tnn - 1) / tnn) * d.batch;
+    if (!e8 && !big && d.variant != 3 && d.variant < 10) continue;
+    const int tnn = e8 ? 256 : w;
+    const long long tiles = (long long)((d.M + tmr - 1) / tmr) * ((d.N + tnn - 1) / tnn) * d.batch;
     // ring kernels, measured: 4096^3 at 1.06 PF/s = 1.94 us per 256x256 k-tile per CU; the
     // 256x128 tile does half the MFMA work per k-tile in ~1.5 us (profiles/r2/gemm_ab_tile_n.txt);
     // 192-row tiles interpolated (a fixed ~1.1 us per k-tile plus ~0.1 us per 32x32 block).
-    // twin: two resident 128x128 workgroups per CU, t_kt per k-tile of one of them, epilogue
-    // and prologue mostly hidden behind the co-resident workgroup
-    const double t_kt = twin ? 0.55e-6 : tmr == 192 ? (w == 256 ? 1.7e-6 : 1.4e-6) : (w == 256 ? 1.9e-6 : 1.5e-6);
-    const double slots = twin ? 512.0 : 256.0;
-    const double fix = twin ? 1.5 : 3.0;
+    // eight-phase kernel: per 256x256 k-tile (gemm_bf16e.hip)
+    const double t_kt = e8 ? 1.35e-6 : tmr == 192 ? (w == 256 ? 1.7e-6 : 1.4e-6) : (w == 256 ? 1.9e-6 : 1.5e-6);
+    const double fix = 3.0;
     for (int s = 1; s <= (fixed ? 1 : 32); ++s) {
       if (s > 1 && kt / s < 2) break;
       if (s > 1 && (size_t)d.batch * s * d.M * d.N > max_ws) break;
-      const double rounds = std::ceil(tiles * s / slots);
-      double t = rounds * (np * std::ceil((double)kt / s) + fix) * t_kt * (twin ? 2.0 : 1.0);
+      const double rounds = std::ceil(tiles * s / 256.0);
+      double t = rounds * (np * std::ceil((double)kt / s) + fix) * t_kt;
       if (s > 1) t += (double)d.batch * s * d.M * d.N * 8.0 / 4.5e12 + 4e-6;
-      if (t < best * 0.97) { best = t; pl.split = s; pl.tn = w; pl.tm = twin ? TT : tmr; }
+      if (t < best * 0.97) { best = t; pl.split = s; pl.tn = w; pl.tm = tmr; }
     }
   }
   return pl;
@@ -1230,9 +769,9 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   if (gemm_bf16_wide(d)) {
     // tile N: the planner's (gemm_run), 256 for the diagnostic variants of the 256x256 forms
     const bool q = d.variant == 0 || d.variant == 3 || (d.variant >= 10 && d.variant <= 15);
-    p.g.tn = q && (g.tn == 128 || g.tn == TN_TWIN) ? g.tn : 256;
-    p.g.tm = q && p.g.tn != TN_TWIN && g.tm == 192 && !d.at ? 192 : 256;
-    const int tm = p.g.tn == TN_TWIN ? TT : p.g.tm, tn = p.g.tn == TN_TWIN ? TT : p.g.tn;
+    p.g.tn = q && (g.tn == 128 || g.tn == TN_E8) ? g.tn : 256;
+    p.g.tm = q && p.g.tn != TN_E8 && g.tm == 192 && !d.at ? 192 : 256;
+    const int tm = p.g.tm, tn = p.g.tn == TN_E8 ? 256 : p.g.tn;
     p.g.ntm = (d.M + tm - 1) / tm;
     p.g.ntn = (d.N + tn - 1) / tn;
     switch (epi) {

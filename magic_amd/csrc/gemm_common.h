@@ -20,11 +20,26 @@ struct Params {
   long long sA, sB, sC;     // batch strides
   int batch, split, kchunk;
   int ntm, ntn;
-  int tn;                   // bf16 DMA kernels: ring-kernel tile N (256 or 128) or TN_TWIN
+  int tn;                   // bf16 DMA kernels: ring-kernel tile N (256 or 128) or TN_E8
   int tm = 256;             // ... and ring-kernel tile M (256, or 192 for a k-contiguous A)
   GemmEpi epi;
 };
-constexpr int TN_TWIN = 1;  // Params::tn of the 128 x 128 twin kernel (gemm_bf16.hip)
+constexpr int TN_E8 = 2;    // Params::tn of the 256 x 256 eight-phase kernel (gemm_bf16e.hip)
+
+// launch parameters of the bf16-plane kernels (gemm_bf16.hip, gemm_bf16e.hip)
+struct PParams {
+  Params g;                         // shapes, fp32 output, batch/split/tiles, epilogue
+  const unsigned short* A; long long pA;
+  const unsigned short* B; long long pB;
+  int npairs, npairs0;
+  unsigned char pa[6], pb[6];
+  int pab;                          // pa[i] | pb[i] << 2 packed 4 bits per pair (no memory reads)
+  const int* dyn;                   // A residual planes nonzero? (nullptr: use all pairs)
+  int diag;                         // timing diagnostics: bit 0 = no operand copies after the
+                                    // prologue (the k-loop multiplies stale LDS images)
+  unsigned long long* stamps;       // stamped diagnostics builds (ST): 8 slots per workgroup
+                                    // {start, prologue landed, k-loop done, end, stores issued}
+};
 
 // tanh as an odd [13/6] rational in x on [-7.905, 7.905] (clamped beyond, where tanh rounds to
 // +-1): one v_rcp_f32 and FMAs that pair into packed v_pk_fma_f32, relative error < 6e-7
@@ -579,4 +594,9 @@ __device__ __forceinline__ void epilogue(const Params& p, const Tile& t, f32x16 
 }
 
 }  // namespace gemm
+
+// the eight-phase 256 x 256 kernel (gemm_bf16e.hip) for a planned tile (g.tn == TN_E8); te: the
+// row-major LDS epilogue
+hipError_t gemm_bf16e_launch(const gemm::PParams& p, bool at, bool bt, int epi, bool te, hipStream_t st);
+
 }  // namespace mvae

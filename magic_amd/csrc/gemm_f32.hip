@@ -418,6 +418,7 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   p.C = ws; p.ldc = d.N; p.sC = (long long)d.M * d.N;
   p.epi.cp = nullptr;  // planes (and the fp32 output, if any) are written by the reduction
   p.epi.c32 = 1;       // the slabs themselves always
+  p.epi.padw = 0;      // slab rows are N wide (ldc = N): no whole-chunk stores past column N
   hipError_t err = d.valu ? gemm_valu_launch(p, d, EPI_STORE, st)
                  : d.prec != GEMM_F32 ? gemm_bf16_launch(p, d, EPI_STORE, st)
                                       : launch_store(p, d.at, d.bt, d.variant, st);

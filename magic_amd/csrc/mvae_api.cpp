@@ -546,12 +546,11 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   }
   build_schedule(c);
   if (const char* nv = std::getenv("MVAE_NO_VALU"); nv && *nv == '1') c->valu = false;
-  // kernel A/B switch (diagnostics): the bf16 DMA GEMMs are planned on the ring kernels only
-  // (default, MVAE_TWIN=0: the 128x128 twin kernel measured slower on every step shape, e.g. C3
-  // 2.263 vs 2.331 ms/step with the planner's twin choices, profiles/r3/README.md); MVAE_TWIN=1
-  // lets the planner choose it, 2 forces it wherever a ring kernel would run
-  int twin_mode = 0;
-  if (const char* tw = std::getenv("MVAE_TWIN"); tw && (*tw == '1' || *tw == '2')) twin_mode = *tw - '0';
+  // kernel A/B switch (diagnostics), MVAE_E8: the 256-row bf16 DMA GEMMs are planned over the
+  // eight-phase and ring kernels (default, 1), on the ring kernels only (0), or on the
+  // eight-phase kernel wherever a 256-row kernel would run (2)
+  int e8_mode = 1;
+  if (const char* e8 = std::getenv("MVAE_E8"); e8 && (*e8 == '0' || *e8 == '2')) e8_mode = *e8 - '0';
   bool dact_planes = true;  // MVAE_DACT_F32AUX=1: bf16-mode DACT reads the fp32 activations (A/B)
   if (const char* fa = std::getenv("MVAE_DACT_F32AUX"); fa && *fa == '1') dact_planes = false;
   const int gp = cfg->precision == MVAE_PREC_BF16 ? GEMM_BF16
@@ -610,8 +609,8 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     // latent head, thin decoder layers) run faster as one native fp32 MFMA GEMM than as six
     // bf16 plane products on the 128x128 kernel; same accuracy class
     if (gp == GEMM_F32X && !gemm_bf16_wide(d)) d.prec = GEMM_F32;
-    if (d.prec != GEMM_F32 && !d.valu && gemm_bf16_wide(d) && twin_mode != 1)
-      d.variant = twin_mode == 0 ? 15 : 13;
+    if (d.prec != GEMM_F32 && !d.valu && gemm_bf16_wide(d) && e8_mode != 1)
+      d.variant = e8_mode == 0 ? 15 : 13;
     // bf16 mode: a plane-kernel DACT epilogue reads the activation's bf16 plane (act' from the
     // bf16-rounded output, the operand precision of this mode), so the forward epilogues write
     // the activations as planes only (no fp32 copy)
@@ -1534,7 +1533,7 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   float ms = 0.f;
   if (e == hipSuccess) e = hipEventElapsedTime(&ms, t0, t1);
   *avg_ms = ms / iters;
-  // MVAE_STAMPS=1 (diagnostics): one more launch of the stamped twin-kernel build (ACT epilogue),
+  // MVAE_STAMPS=1 (diagnostics): one more launch of the stamped ring-kernel build,
   // per-workgroup segment times (us, 100 MHz stamps) summarised on stderr
   if (const char* sp = std::getenv("MVAE_STAMPS"); e == hipSuccess && sp && *sp == '1') {
     const int nmax = 1 << 20;

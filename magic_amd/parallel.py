@@ -15,10 +15,16 @@ Per step and rank (``world`` ranks, local batch B, global batch N*B):
                                        xGMI on MI355X) while the later parts run, then
                                        waited on
   adam()                               identical on every rank -> replicas stay bitwise equal
-  all_reduce(losses) (optional)        5 floats, for logging / the NaN guard
+  all_reduce(losses) (optional)        5 floats, for logging / the NaN guard: issued async
+                                       right after metric() so it runs beside the backward,
+                                       waited for at the end of the step -- colsq / coldot
+                                       are the only blocking collectives of a cosine step
 
 The squared-difference metric needs no mid-step collective; the result equals the
-single-process step on the concatenated batch (tests/test_parallel_gloo.py).
+single-process step on the concatenated batch (tests/test_parallel_gloo.py) to fp32
+rounding: with more than one rank the layer-0 weight gradient runs as ``wgrad0_chunks`` row
+chunks (engine option, set here and restored by ``close()``), whose GEMMs plan their own
+split-K, so those rows are not bitwise equal to a single-process one-GEMM backward.
 """
 from __future__ import annotations
 
@@ -48,10 +54,12 @@ class DataParallelStep:
             raise ValueError(f"engine global_batch {engine.cfg.gbatch} != batch {engine.cfg.batch} "
                              f"x world {self.world}")
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self._chunks_set = False
         if self.coll and self.overlap and hasattr(engine, "set_option"):
             # the layer-0 weight gradient (40 MB of the 69 MB bucket at C4) in 4 row chunks, each
             # all-reduced while the next computes, instead of one transfer after the last GEMM
             engine.set_option("wgrad0_chunks", wgrad0_chunks)
+            self._chunks_set = True
         if hasattr(engine, "set_shard"):
             # the internal eps sampler draws this rank's rows of the global batch's stream,
             # so a sharded step without explicit eps equals the single-process step too
@@ -61,12 +69,22 @@ class DataParallelStep:
         if self.coll:
             dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
 
+    def close(self):
+        """Restore the engine's one-GEMM layer-0 weight gradient (single-process rounding)."""
+        if self._chunks_set:
+            self.e.set_option("wgrad0_chunks", 1)
+            self._chunks_set = False
+
     def step(self, x, areas, eps=None):
         e = self.e
         e.forward(x, eps)
         if self.cosine:
             self._ar(e.colsq)
         e.metric(areas)
+        # the 5 loss sums are final after metric(): reduce them beside the backward
+        h_loss = None
+        if self.reduce_losses and self.coll:
+            h_loss = dist.all_reduce(e.losses, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         if self.cosine:
             self._ar(e.coldot)
         if self.coll and self.overlap:
@@ -82,8 +100,8 @@ class DataParallelStep:
             e.backward()
             self._ar(e.grads)
         e.adam()
-        if self.reduce_losses:
-            self._ar(e.losses)
+        if h_loss is not None:
+            h_loss.wait()
         return e.losses
 
 

@@ -165,9 +165,11 @@ class TangoEncoder(object):
 
 def sample_latent_space(vae, nx: int = 20, ny: int = 20, lo: float = -3.0, hi: float = 3.0):
     """The 2-D latent-space sampling grid of ``11a/utils.py:401-422`` as an array (the reference
-    plots it to a PNG; plotting is out of scope): an (ny*S) x (nx*S) canvas, S = image side, tile
-    (nx - i - 1, j) = ``vae.generate`` of z = (v[j], v[i]) with v = linspace(lo, hi, nx), as the
-    reference's loop over ``yi in x_values`` / ``xi in y_values`` places it. The reference runs one
+    plots it to a PNG; plotting is out of scope): tile (nx - i - 1, j) = ``vae.generate`` of
+    z = (w[j], v[i]) with v = linspace(lo, hi, nx), w = linspace(lo, hi, ny), as the reference's
+    loop over ``yi in x_values`` / ``xi in y_values`` places it, so the canvas is nx tiles tall
+    and ny tiles wide, (nx*S) x (ny*S) for image side S (the reference hard-codes nx = ny = 20,
+    where its (ny*S) x (nx*S) canvas is the same shape). The reference runs one
     ``generate`` per grid point on a batch of identical rows and keeps row 0; here the grid points
     are the rows of ``ceil(nx*ny / batch_size)`` batched ``generate`` calls. Returns None unless
     the latent space is 2-D (the reference prints a message instead).
@@ -182,7 +184,7 @@ def sample_latent_space(vae, nx: int = 20, ny: int = 20, lo: float = -3.0, hi: f
         rows.append(np.asarray(vae.generate(z[s0:s0 + vae.batch_size])))
     imgs = np.concatenate(rows, axis=0)
     side = int(round(np.sqrt(imgs.shape[1])))
-    canvas = np.empty((side * ny, side * nx), dtype=imgs.dtype)
+    canvas = np.empty((side * nx, side * ny), dtype=imgs.dtype)
     for i in range(len(x_values)):
         for j in range(len(y_values)):
             canvas[(nx - i - 1) * side:(nx - i) * side, j * side:(j + 1) * side] = \

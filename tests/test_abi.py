@@ -81,3 +81,20 @@ def test_build_id_ties_library_to_sources():
     assert any(p.endswith(os.path.join("include", "mvae.h")) for p in source_files())
     with pytest.raises(_lib.MVAELibraryError, match="stale"):
         _lib.verify_build(lib, expected="0" * 16)
+
+
+def test_build_id_ignores_stray_files_and_names_missing_sources(tmp_path, monkeypatch):
+    """Only the compiled sources enter the build id (a stray file under csrc/ does not make the
+    library "stale"); a missing source raises MVAELibraryError naming it, not a bare OSError."""
+    from magic_amd import build
+    lib = _lib.load()
+    stray = os.path.join(build.CSRC, "zz_stray_editor_file.orig")
+    with open(stray, "w") as f:
+        f.write("not a source\n")
+    try:
+        assert _lib.verify_build(lib) == build.source_hash()
+    finally:
+        os.remove(stray)
+    monkeypatch.setattr(build, "SOURCES", build.SOURCES + ["does_not_exist.hip"])
+    with pytest.raises(_lib.MVAELibraryError, match="does_not_exist.hip"):
+        _lib.verify_build(lib)

@@ -141,6 +141,15 @@ def test_sample_latent_space_grid_layout():
             assert tile[0] == np.float32(v[j]) and tile[1] == np.float32(v[i])
     assert sum(f.calls) == 25 and max(f.calls) == 7
 
+    # nx != ny: nx tiles tall (z[1] = v[i]), ny tiles wide (z[0] = w[j])
+    c = sample_latent_space(Fake(), nx=3, ny=4)
+    assert c.shape == (12, 16)
+    v, w = np.linspace(-3, 3, 3), np.linspace(-3, 3, 4)
+    for i in range(3):
+        for j in range(4):
+            tile = c[(3 - i - 1) * 4:(3 - i) * 4, j * 4:(j + 1) * 4].reshape(-1)
+            assert tile[0] == np.float32(w[j]) and tile[1] == np.float32(v[i])
+
     class Fake3(Fake):
         latent_dimensions = 3
 

@@ -16,20 +16,22 @@ from tests.gpu_helpers import make_inputs, make_params, max_rel
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, metric, q, conv=False):
+def _worker(rank, world, port, metric, q, conv=False, size=24, chunks=4):
     import torch.distributed as dist
     from magic_amd.engine import Engine
     from magic_amd.parallel import DataParallelStep
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    cfg = preset("8c", image_size=24, batch=32, metric=metric, conv=conv)
+    cfg = preset("8c", image_size=size, batch=32, metric=metric, conv=conv)
     B = cfg.batch
     half = B // world
     eng = Engine(cfg.replace(batch=half, global_batch=B), 0)
     eng.load_params(make_params(cfg))
     X, areas, eps = make_inputs(cfg, B)
     sl = slice(rank * half, (rank + 1) * half)
-    st = DataParallelStep(eng)
+    st = DataParallelStep(eng, wgrad0_chunks=chunks)
+    if chunks > 1:
+        assert eng.N_BACKWARD_PARTS > 3  # the layer-0 weight gradient really runs in row chunks
     st.step(torch.from_numpy(X[sl]).cuda(), torch.from_numpy(areas[sl]).cuda(),
             torch.from_numpy(np.ascontiguousarray(eps[:, sl])).cuda())
     torch.cuda.synchronize()
@@ -38,12 +40,16 @@ def _worker(rank, world, port, metric, q, conv=False):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("metric,conv", [("cosine", False), ("sqdiff", False), ("sqdiff", True)])
-def test_dp2_on_gpu_matches_full_batch(metric, conv):
+@pytest.mark.parametrize("metric,conv,size,chunks", [("cosine", False, 24, 4), ("sqdiff", False, 24, 4),
+                                                     ("sqdiff", True, 24, 4), ("cosine", False, 48, 4),
+                                                     ("cosine", False, 48, 1)])
+def test_dp2_on_gpu_matches_full_batch(metric, conv, size, chunks):
+    """2 ranks (async loss all-reduce beside the backward; layer-0 weight gradient in
+    ``wgrad0_chunks`` row chunks, each all-reduced as it completes) vs one process."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from magic_amd.engine import Engine
-    cfg = preset("8c", image_size=24, batch=32, metric=metric, conv=conv)
+    cfg = preset("8c", image_size=size, batch=32, metric=metric, conv=conv)
     eng = Engine(cfg, 0)
     eng.load_params(make_params(cfg))
     X, areas, eps = make_inputs(cfg, cfg.batch)
@@ -60,7 +66,7 @@ def test_dp2_on_gpu_matches_full_batch(metric, conv):
     s.close()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, metric, q, conv)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, metric, q, conv, size, chunks)) for r in range(2)]
     for p in procs:
         p.start()
     res = dict((r, (g, l)) for r, g, l in (q.get(timeout=300) for _ in range(2)))

@@ -1,7 +1,8 @@
-"""GPU parity for the round-3 items: the 128x128 twin GEMM kernel (two workgroups per CU) on
-every operand layout, ragged edge and fused epilogue, and whole training steps with the twin
-kernel forced onto every bf16 DMA GEMM (MVAE_TWIN=2) or excluded (MVAE_TWIN=0), against the
-float64 oracle at the fp32 bar (f32x) and the documented bf16 bar."""
+"""GPU parity for the eight-phase 256x256 GEMM kernel (gemm_bf16e.hip, round 4) on every
+operand layout, ragged edge and fused epilogue, and whole training steps with it forced onto
+every 256-row bf16 DMA GEMM (MVAE_E8=2) or excluded (MVAE_E8=0), against the float64 oracle at
+the fp32 bar (f32x) and the documented bf16 bar; plus the round-3 items (chunked layer-0
+gradient, 192-row ring tiles, latent sampling grid)."""
 import pytest
 import torch
 
@@ -20,15 +21,17 @@ def _need_gpu():
         pytest.skip("no GPU")
 
 
-# ------------------------------------------------------------------ twin kernel
+# ------------------------------------------------------------------ eight-phase kernel
 @pytest.mark.parametrize("prec", [2, 1], ids=["f32x", "bf16"])
 @pytest.mark.parametrize("at,bt", [(0, 0), (1, 0), (0, 1), (1, 1)])
 @pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 13), (300, 517, 1001, 13), (1000, 600, 4099, 13),
                                            (513, 260, 130, 14), (40, 70, 200, 13), (2100, 500, 700, 14),
-                                           (129, 40, 8193, 13), (1, 8, 1, 13)])
-def test_gemm_twin_kernel(at, bt, M, N, K, variant, prec):
-    """Variant 13 / 14 force the twin kernel (14 also routes fp32-only outputs through its LDS
-    row-major epilogue); ragged M / N / K edges and the planner's split-K (K 4099, 8193)."""
+                                           (129, 40, 8193, 13), (1, 8, 1, 13), (256, 256, 192, 13),
+                                           (520, 770, 320, 13)])
+def test_gemm_e8_kernel(at, bt, M, N, K, variant, prec):
+    """Variant 13 / 14 force the eight-phase kernel (14 also routes fp32-only outputs through its
+    LDS row-major epilogue); ragged M / N / K edges, tiles smaller than 256 x 256, odd k-tile
+    counts (the pipeline's tail waits) and the planner's split-K (K 4099, 8193)."""
     lib = _lib.load()
     g = torch.Generator(device="cuda").manual_seed(M * 5 + N * 11 + K + variant)
     A = _padded(K, M, g) if at else _padded(M, K, g)
@@ -51,8 +54,8 @@ def test_gemm_twin_kernel(at, bt, M, N, K, variant, prec):
 @pytest.mark.parametrize("epi,act", [(1, 0), (1, 1), (2, 0), (2, 1), (4, 0)])
 @pytest.mark.parametrize("M,N,ldc", [(600, 520, 520), (300, 500, 500), (130, 257, 264), (280, 300, 301)])
 @pytest.mark.parametrize("variant,planes", [(13, 0), (13, 1), (14, 0)])
-def test_gemm_twin_epilogues(prec, epi, act, M, N, ldc, variant, planes):
-    """Fused ACT / DACT / SIGMOID epilogues of the twin kernel against float64, in both its
+def test_gemm_e8_epilogues(prec, epi, act, M, N, ldc, variant, planes):
+    """Fused ACT / DACT / SIGMOID epilogues of the eight-phase kernel against float64, in both its
     epilogue forms (C/D layout; LDS row-major with 16-B stores and element tails, ld 301 falls
     back to the C/D layout); nothing written past column N."""
     lib = _lib.load()
@@ -86,13 +89,14 @@ def test_gemm_twin_epilogues(prec, epi, act, M, N, ldc, variant, planes):
         assert torch.isnan(C[:, N:]).all()
 
 
-@pytest.mark.parametrize("mode", ["0", "2"], ids=["ring_only", "twin_everywhere"])
+@pytest.mark.parametrize("mode", ["0", "2"], ids=["ring_only", "e8_everywhere"])
 @pytest.mark.parametrize("prec", ["f32x", "bf16"])
 @pytest.mark.parametrize("grey", [False, True], ids=["binary", "grey"])
-def test_step_twin_modes(monkeypatch, mode, prec, grey):
-    """A whole step with every bf16 DMA GEMM on the twin kernel (BCE head with fp32 or bf16-plane
-    target, DACT row remap, batch-2 weight gradients, split-K) or on the ring kernels only."""
-    monkeypatch.setenv("MVAE_TWIN", mode)
+def test_step_e8_modes(monkeypatch, mode, prec, grey):
+    """A whole step with every 256-row bf16 DMA GEMM on the eight-phase kernel (BCE head with fp32
+    or bf16-plane target, DACT row remap, batch-2 weight gradients, split-K) or on the ring
+    kernels only."""
+    monkeypatch.setenv("MVAE_E8", mode)
     cfg = preset("8c", image_size=20, batch=288, precision=prec).replace(enc=(300, 260, 280))
     if prec == "f32x":
         check_step(cfg, grey=grey, recon=True)
@@ -100,18 +104,18 @@ def test_step_twin_modes(monkeypatch, mode, prec, grey):
         check_step(cfg, grey=grey, recon=True, **BF16)
 
 
-@pytest.mark.parametrize("mode", ["1", "2"], ids=["planner", "twin_everywhere"])
-def test_step_c3_shape_twin(monkeypatch, mode):
+@pytest.mark.parametrize("mode", ["1", "2"], ids=["planner", "e8_everywhere"])
+def test_step_c3_shape_e8(monkeypatch, mode):
     """BASELINE C3's shapes (8d, bf16, 100x100, enc [500]*4, L = 200) at B = 2048 with the default
-    plan and with the twin kernel everywhere, documented bf16 bar."""
-    monkeypatch.setenv("MVAE_TWIN", mode)
+    plan and with the eight-phase kernel everywhere, documented bf16 bar."""
+    monkeypatch.setenv("MVAE_E8", mode)
     check_step(baseline_config("C3").replace(batch=2048), adam=False, **BF16)
 
 
-def test_step_c2_f32x_twin_everywhere(monkeypatch):
-    """The benched C2 configuration (f32x, B = 4096) with the twin kernel on every bf16 GEMM, at the
-    fp32 bar."""
-    monkeypatch.setenv("MVAE_TWIN", "2")
+def test_step_c2_f32x_e8_everywhere(monkeypatch):
+    """The benched C2 configuration (f32x, B = 4096) with the eight-phase kernel on every 256-row
+    bf16 GEMM, at the fp32 bar."""
+    monkeypatch.setenv("MVAE_E8", "2")
     check_step(preset("8c", image_size=100, batch=4096, precision="f32x"), adam=False)
 
 

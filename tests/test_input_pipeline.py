@@ -69,6 +69,31 @@ def test_hip_batch_producer_bit_exact():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("h,w", [(200, 200), (100, 100), (199, 197), (64, 36)],
+                         ids=["vec_200", "vec_100_partial_segment", "scalar_odd", "vec_small"])
+@pytest.mark.parametrize("normalize", [True, False], ids=["div255", "raw"])
+def test_hip_batch_producer_paths(h, w, normalize):
+    """Both kernel paths (4 pixels per thread through LDS when H*W % 4 == 0, else one pixel per
+    thread) bit-exact against the oracle, on grey uint8 tables (every byte value, so every
+    quotient v/255 occurs) and raw 0..255 output."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from magic_amd.overlap_input import make_batch, rotation_coefficients
+    rng = np.random.default_rng(h * 7 + w)
+    n, B = 7, 33
+    L = rng.integers(0, 256, (n, h, w), dtype=np.uint8)
+    K = rng.integers(0, 256, (n, h, w), dtype=np.uint8)
+    idx = rng.integers(0, n, B).astype(np.int32)
+    ang = rng.uniform(0, 2 * math.pi, B).astype(np.float32)
+    ang[:3] = [0.0, math.pi / 2, math.pi]
+    coef = rotation_coefficients(ang, h, w)
+    X = make_batch(torch.from_numpy(L).cuda(), torch.from_numpy(K).cuda(), torch.from_numpy(idx).cuda(),
+                   torch.from_numpy(coef).cuda(), normalize=normalize).cpu().numpy()
+    ref = IO.make_batch(L, K, idx, coef, scale_div=255.0 if normalize else 1.0)
+    np.testing.assert_array_equal(X, ref)
+
+
+@pytest.mark.gpu
 def test_batch_stream_on_reference_images():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
