@@ -201,14 +201,9 @@ def _csv_rows(d, suffix):
     return out
 
 
-def _region_counter(d, counter, region_ids):
-    """Mean per launch of `counter` (summed over the dispatches between each pair of marker
-    kernels of a region) for every region id, from one rocprofv3 output directory."""
-    vals = {}
-    for r in _csv_rows(d, "counter_collection.csv"):
-        if r.get("Counter_Name") == counter:
-            k = int(r["Dispatch_Id"])
-            vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
+def _region_dispatches(d, region_ids):
+    """For every region id: the lists of kernel-trace rows between each pair of its marker
+    kernels (one list per bracketed launch), from one rocprofv3 output directory."""
     trace = sorted(_csv_rows(d, "kernel_trace.csv"), key=lambda r: int(r["Dispatch_Id"]))
     from magic_amd._lib import MARKER_GRID
 
@@ -217,7 +212,7 @@ def _region_counter(d, counter, region_ids):
         return g // max(1, int(r.get("Workgroup_Size_X") or r.get("Workgroup_Size") or 1))
     out = {}
     for rid in region_ids:
-        sums, open_ = [], None
+        groups, open_ = [], None
         for r in trace:
             if "mvae_region_marker" in r["Kernel_Name"]:
                 if wgs(r) != MARKER_GRID + rid:
@@ -227,20 +222,49 @@ def _region_counter(d, counter, region_ids):
                 else:
                     lo, q = open_
                     hi = int(r["Dispatch_Id"])
-                    ids = [int(x["Dispatch_Id"]) for x in trace
-                           if lo < int(x["Dispatch_Id"]) < hi and x.get("Queue_Id") == q
-                           and "mvae_region_marker" not in x["Kernel_Name"]]
-                    sums.append(sum(vals.get(i, 0.0) for i in ids))
+                    groups.append([x for x in trace if lo < int(x["Dispatch_Id"]) < hi and x.get("Queue_Id") == q
+                                   and "mvae_region_marker" not in x["Kernel_Name"]])
                     open_ = None
-        if sums:
-            out[rid] = sum(sums) / len(sums)
+        if groups:
+            out[rid] = groups
     return out
 
 
-def pmc_traffic(args, names, regions_all):
+def _region_counter(d, counter, region_ids):
+    """Mean per launch of `counter` (summed over the dispatches between each pair of marker
+    kernels of a region) for every region id, from one rocprofv3 output directory."""
+    vals = {}
+    for r in _csv_rows(d, "counter_collection.csv"):
+        if r.get("Counter_Name") == counter:
+            k = int(r["Dispatch_Id"])
+            vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
+    out = {}
+    for rid, groups in _region_dispatches(d, region_ids).items():
+        sums = [sum(vals.get(int(x["Dispatch_Id"]), 0.0) for x in g) for g in groups]
+        out[rid] = sum(sums) / len(sums)
+    return out
+
+
+def _region_ns(d, region_ids):
+    """Mean summed kernel duration (ns) per bracketed launch of each region."""
+    out = {}
+    for rid, groups in _region_dispatches(d, region_ids).items():
+        t = [sum(int(x["End_Timestamp"]) - int(x["Start_Timestamp"]) for x in g) for g in groups]
+        out[rid] = sum(t) / len(t)
+    return out
+
+
+N_SIMD = 1024  # 256 CUs x 4 SIMDs (MI355X)
+
+
+def pmc_traffic(args, names, regions_all, config=None, mfma=()):
     """HBM bytes per launch of each region in `names`: two rocprofv3 child runs of this bench
     (FETCH_SIZE and WRITE_SIZE cannot share a pass), markers around the regions; FETCH_SIZE x2
-    (gfx950 reports half of a wide streaming read) and KB -> B."""
+    (MI355X_MICROARCH.md: gfx950 reports half of a wide streaming read) and KB -> B. For the
+    regions in `mfma`, a third pass (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE): the matrix-pipe
+    busy fraction over the kernels' own cycles, mfma_busy = MFMA-busy cycles / (N_SIMD x
+    GRBM_GUI_ACTIVE / 8) (GRBM_GUI_ACTIVE is summed over the 8 XCDs), and the clock the chip held,
+    (GRBM_GUI_ACTIVE / 8) / kernel time."""
     exe = shutil.which("rocprofv3")
     if not exe:
         return None, "rocprofv3 not on PATH"
@@ -249,20 +273,23 @@ def pmc_traffic(args, names, regions_all):
         else tempfile.gettempdir()
     root = tempfile.mkdtemp(prefix="bench_pmc_", dir=base)
     child = [sys.executable, os.path.abspath(__file__), "--pmc-child", ",".join(str(r) for r in ids.values()),
-             "--config", args.config, "--steps", "2", "--warmup", "1"]
-    if args.batch:
+             "--config", config or args.config, "--steps", "2", "--warmup", "1"]
+    if args.batch and config is None:
         child += ["--batch", str(args.batch)]
-    if args.precision:
+    if args.precision and config is None:
         child += ["--precision", args.precision]
     for o in args.opt:
         child += ["--opt", o]
-    res = {}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        d = os.path.join(root, counter.lower())
-        cmd = [exe, "--pmc", counter, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run",
+    passes = [("fetch", ["FETCH_SIZE"]), ("write", ["WRITE_SIZE"])]
+    if mfma:
+        passes.append(("mfma", ["SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]))
+    res, ns = {}, {}
+    for tag, counters in passes:
+        d = os.path.join(root, tag)
+        cmd = [exe, "--pmc", *counters, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run",
                "--", *child]
         env = dict(os.environ, TMPDIR="/tmp")
-        with open(os.path.join(root, counter.lower() + ".log"), "w") as log:
+        with open(os.path.join(root, tag + ".log"), "w") as log:
             p = subprocess.Popen(cmd, cwd="/tmp", env=env, stdout=log, stderr=subprocess.STDOUT,
                                  start_new_session=True)
             try:
@@ -270,17 +297,32 @@ def pmc_traffic(args, names, regions_all):
             except subprocess.TimeoutExpired:
                 os.killpg(p.pid, signal.SIGKILL)
                 p.wait()
-                return None, f"{counter} pass timed out"
+                return None, f"{tag} pass timed out"
         if rc != 0:
-            return None, f"{counter} pass rc={rc} (log {root})"
-        res[counter] = _region_counter(d, counter, list(ids.values()))
+            return None, f"{tag} pass rc={rc} (log {root})"
+        for c in counters:
+            res[c] = _region_counter(d, c, list(ids.values()))
+        if tag == "mfma":
+            ns = _region_ns(d, list(ids.values()))
     out = {}
     for n, rid in ids.items():
         f, w = res["FETCH_SIZE"].get(rid), res["WRITE_SIZE"].get(rid)
         if f is not None and w is not None:
             out[n] = {"hbm_bytes": round(f * 1024 * 2 + w * 1024),
                       "fetch_bytes": round(f * 1024 * 2), "write_bytes": round(w * 1024)}
-    return out, f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE child passes, marker-bracketed ({root})"
+        busy, gui = res.get("SQ_VALU_MFMA_BUSY_CYCLES", {}).get(rid), res.get("GRBM_GUI_ACTIVE", {}).get(rid)
+        if n in mfma and busy and gui:
+            cyc = gui / 8.0
+            e = out.setdefault(n, {})
+            e["mfma_busy"] = round(busy / (N_SIMD * cyc), 4)
+            e["mfma_busy_cycles"] = round(busy)
+            e["kernel_cycles"] = round(cyc)
+            if ns.get(rid):
+                e["clock_ghz"] = round(cyc / ns[rid], 3)
+                e["profiled_ms"] = round(ns[rid] / 1e6, 4)
+    return out, (f"rocprofv3 child passes of this bench ({config or args.config}), marker-bracketed: "
+                 f"--pmc FETCH_SIZE / WRITE_SIZE" + (" / SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE" if mfma else "")
+                 + f" ({root})")
 
 
 # ------------------------------------------------------------------------ CPU baseline
@@ -808,10 +850,27 @@ def main():
                 continue
             c = config_of("C3" if cid == "C4" else cid, small=args.dry_run)
             m = measure(args, c, world, rank, local, dev, timing=timing, steps=args.steps,
-                        warmup=args.warmup, pipeline=not args.no_pipeline)
+                        warmup=args.warmup, pipeline=not args.no_pipeline, keep=True)
+            ce = m.pop("eng", None)
+            names_c = ce.timing_names() if hasattr(ce, "timing_names") else []
+            if ce is not None:
+                ce.close()
             if rank == 0:
                 print_regions(args, m, cid)
                 rf, lr = rooflines(args, m)
+                # the config's own HBM traffic and MFMA-busy counters (same passes as the headline)
+                if rf and world == 1 and args.pmc == "auto" and not args.dry_run:
+                    want = [m["dom"]] + [k for k in PMC_REGIONS_BW if k in m["regions"]]
+                    tr, how = pmc_traffic(args, want, names_c, config=cid, mfma=(m["dom"],))
+                    rf["traffic_method"] = how
+                    if tr and m["dom"] in tr:
+                        rf["traffic"] = tr[m["dom"]].get("hbm_bytes")
+                        rf["traffic_detail"] = tr[m["dom"]]
+                        if "mfma_busy" in tr[m["dom"]]:
+                            rf["mfma_busy"] = tr[m["dom"]]["mfma_busy"]
+                    for k in PMC_REGIONS_BW:
+                        if tr and k in tr and lr and k in lr and "hbm_bytes" in tr[k]:
+                            lr[k]["traffic"] = tr[k]["hbm_bytes"]
                 extra[cid] = {"workload": workload("C3" if cid == "C4" else cid, c) +
                               (f" x {world} ranks" if world > 1 else ""),
                               "value": round(c.batch * world * m["steps"] / m["elapsed"], 2),
@@ -831,12 +890,14 @@ def main():
         if roofline and world == 1 and args.pmc == "auto" and not args.dry_run:
             names = eng.timing_names()
             want = [head["dom"]] + [k for k in PMC_REGIONS_BW if k in head["regions"]]
-            tr, how = pmc_traffic(args, want, names)
+            tr, how = pmc_traffic(args, want, names, mfma=(head["dom"],))
             roofline["traffic_method"] = how
             if tr:
                 if head["dom"] in tr:
-                    roofline["traffic"] = tr[head["dom"]]["hbm_bytes"]
+                    roofline["traffic"] = tr[head["dom"]].get("hbm_bytes")
                     roofline["traffic_detail"] = tr[head["dom"]]
+                    if "mfma_busy" in tr[head["dom"]]:
+                        roofline["mfma_busy"] = tr[head["dom"]]["mfma_busy"]
                 for k in PMC_REGIONS_BW:
                     if k in tr and k in loss_roofline:
                         loss_roofline[k]["traffic"] = tr[k]["hbm_bytes"]

@@ -612,15 +612,15 @@ bool wide_epi_vec_ok(const Params& g) {
 // interleaved ring kernel. Their epilogue goes through LDS (row-major 16-B stores) when the tile
 // writes bf16 planes or is the BCE head (2-B plane stores and 4-B target loads per element
 // otherwise), and stays in the C/D layout for fp32-only outputs (split-K slabs: 128-B row
-// segments already, where the LDS round trip measured 5-10 % slower); variant 14 routes
-// fp32-only outputs of the eight-phase kernel through LDS too, variant 10 keeps the ring kernel
-// on the C/D layout.
+// segments already, where the LDS round trip measured 5-10 % slower); the eight-phase kernel's
+// accumulators are not in the C/D row-segment order, so its epilogue always goes through LDS
+// (variant 14 = 13); variant 10 keeps the ring kernel on the C/D layout.
 template <int EPI>
 hipError_t launch_wide(const PParams& p, bool at, bool bt, int variant, hipStream_t st) {
   constexpr bool BCE = EPI == EPI_BCE || EPI == EPI_BCEB;
-  if (p.g.tn == TN_E8) {
-    const bool te = (p.g.epi.cp || BCE || variant == 14) && wide_epi_vec_ok(p.g);
-    return gemm_bf16e_launch(p, at, bt, EPI, te, st);
+  if (p.g.tn == TN_E8) {  // always the LDS epilogue: 16-B accesses where aligned, else element-wise
+    (void)variant;
+    return gemm_bf16e_launch(p, at, bt, EPI, wide_epi_vec_ok(p.g), st);
   }
   if ((p.g.epi.cp || BCE) && variant != 10 && wide_epi_vec_ok(p.g))
     return launch_q_t<EPI, true>(p, at, bt, st);
@@ -660,10 +660,11 @@ hipError_t launch_var(const PParams& p, bool at, bool bt, int variant, hipStream
 bool gemm_bf16_wide(const GemmDesc& d) {
   if (d.prec == GEMM_F32) return false;
   // 10-12, 15: default-shape variants of the ring kernel (C/D epilogue, forced tile N, no
-  // eight-phase kernel); 3: the ring kernel, 13 / 14: the eight-phase kernel, on any shape
+  // eight-phase kernel); 3: the ring kernel, 13 / 14: the eight-phase kernel (5 / 6: with the
+  // 16x16x32 / 32x32x16 MFMA), on any shape
   const int v = (d.variant >= 10 && d.variant != 13 && d.variant != 14) ? 0 : d.variant;
   if (v == 1 || v == 2 || v == 4) return false;  // 128x128 register-staged variants
-  if (v != 3 && v != 13 && v != 14 && (d.M < 256 || d.N < 256)) return false;
+  if (v != 3 && v != 5 && v != 6 && v != 13 && v != 14 && (d.M < 256 || d.N < 256)) return false;
   // one k-tile and under a CU's worth of 256x256 tiles (dec layer 1: K = L + 1; the head's
   // dgrad: K = 2L): epilogue-bound on few CUs, the 128x128 kernels spread it wider
   const long long t256 = (long long)((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
@@ -698,7 +699,7 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
     for (int j = 0; j < d.nB; ++j) np += i + j < T;
   if (d.dynA) np = (np + (d.nB < T ? d.nB : T)) / 2;  // A's residual planes often all zero
   const bool big = d.M >= 256 && d.N >= 256;
-  const bool force_e8 = d.variant == 13 || d.variant == 14;
+  const bool force_e8 = d.variant == 13 || d.variant == 14 || d.variant == 5 || d.variant == 6;
   const bool allow_e8 = force_e8 || (d.variant == 0 && big);
   double best = 1e30;
   WidePlan pl;
@@ -747,9 +748,20 @@ void gemm_bf16_wide_plan(const GemmDesc& d, size_t max_ws, int* split, int* tn, 
   *split = pl.split; *tn = pl.tn; *tm = pl.tm;
 }
 
+// MVAE_E8_MF (A/B): the eight-phase kernel's MFMA shape, 16 = v_mfma_f32_16x16x32_bf16,
+// otherwise 32x32x16
+static int e8_mf() {
+  static const int mf = [] {
+    const char* v = std::getenv("MVAE_E8_MF");
+    return v && std::atoi(v) == 16 ? 16 : 32;
+  }();
+  return mf;
+}
+
 hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, hipStream_t st) {
   PParams p;
   p.g = g;
+  p.mf = d.variant == 5 ? 16 : d.variant == 6 ? 32 : e8_mf();
   p.A = d.Ap; p.pA = d.pA;
   p.B = d.Bp; p.pB = d.pB;
   p.dyn = d.dynA;
@@ -768,7 +780,8 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   for (int i = 0; i < n; ++i) p.pab |= (p.pa[i] | p.pb[i] << 2) << (4 * i);
   if (gemm_bf16_wide(d)) {
     // tile N: the planner's (gemm_run), 256 for the diagnostic variants of the 256x256 forms
-    const bool q = d.variant == 0 || d.variant == 3 || (d.variant >= 10 && d.variant <= 15);
+    const bool q = d.variant == 0 || d.variant == 3 || d.variant == 5 || d.variant == 6 ||
+                   (d.variant >= 10 && d.variant <= 15);
     p.g.tn = q && (g.tn == 128 || g.tn == TN_E8) ? g.tn : 256;
     p.g.tm = q && p.g.tn != TN_E8 && g.tm == 192 && !d.at ? 192 : 256;
     const int tm = p.g.tm, tn = p.g.tn == TN_E8 ? 256 : p.g.tn;

@@ -36,6 +36,7 @@ using namespace gemm;
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) short lds_short;
 
 constexpr int EBK = 64;          // k-tile
@@ -47,22 +48,24 @@ constexpr int ENT = 512;
 // operand's plane, 2 GB range): per lane only a 32-bit byte offset; the k-tile's offset is the
 // scalar soffset, and chunks that must read as zero (past K, or row chunks past the operand's
 // rows) take an offset past the resource's range, which the hardware returns as zeros.
-// Image row i (0..127) of half h is tile row map(i, h): SUB rows of each wave slice (A: 2 wave
-// rows x 64, B: 4 wave columns x 32). Each lane copies 2 16-B chunks per half (8 waves x 64
-// lanes x 2 = 1024 chunks = 16 KB):
+// Image row i (0..127) of half h is tile row (column, for B) 128 h + i, so a row-contiguous
+// operand's DMA reads whole 256-B row segments. Each lane copies 2 16-B chunks per half (8 waves
+// x 64 lanes x 2 = 1024 chunks = 16 KB):
 //   k-contiguous ([rows][K] in HBM): image [128 rows][8 chunks of 8 k], chunk c of row i stored
 //     at c ^ ((i >> 1) & 7) -> ds_read_b128 fragment reads conflict-free;
 //   row-contiguous ([K][rows]): image [64 k][16 chunks of 8 rows], chunk c of k-row k stored
-//     at c ^ (4 (k & 3)) -> the 32 lanes of a ds_read_b64_tr_b16 pass hit 32 distinct slots.
+//     at c ^ tr_swz(k) -> the 32 lanes of a ds_read_b64_tr_b16 pass hit 32 distinct slots.
 // Rows past the end of a k-contiguous operand are clamped (their outputs are not stored).
 constexpr unsigned OOB = 0x80000000u;  // >= the resource's num_records: loads zeros
-template <bool KC, int SUB>
+// chunk swizzle of a row-contiguous image's k-row k: the 4 (k & 3) term spreads the four k-rows
+// of one ds_read_b64_tr_b16 block, the 2 ((k >> 3) & 1) term the two 8-row-apart blocks a
+// 32-lane half of the 16x16x32 B-operand read takes in the same columns (both conflict-free)
+__device__ __forceinline__ int tr_swz(int k) { return (4 * (k & 3)) ^ (2 * ((k >> 3) & 1)); }
+template <bool KC>
 struct HLoad {
   unsigned voff[2][2];  // [chunk j][half h]: byte offset of the chunk at k0 = 0, or OOB
   int kc[2];            // its k within the tile (k-contiguous: 8c; else the k row)
-  __device__ __forceinline__ static int map(int i, int h) {
-    return (i / SUB) * (2 * SUB) + h * SUB + (i % SUB);
-  }
+  __device__ __forceinline__ static int map(int i, int h) { return h * 128 + i; }
   __device__ __forceinline__ void init(int ld, int r0, int nrows, int wave, int lane) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -78,7 +81,7 @@ struct HLoad {
           kc[j] = 8 * c;
         } else {
           const int krow = q >> 4;
-          const int c = (q & 15) ^ (4 * (krow & 3));
+          const int c = (q & 15) ^ tr_swz(krow);
           const int col = r0 + map(8 * c, h);
           voff[j][h] = col < nrows ? 2u * ((unsigned)krow * (unsigned)ld + (unsigned)col) : OOB;
           kc[j] = krow;
@@ -120,20 +123,34 @@ __device__ __forceinline__ bf16x8 rd_tr(unsigned a) {
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a), "i"(OFF + 4 * 256));
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
-// per-lane byte offset within a half image of the fragment of the 32-row block at image row
-// rb, k16-step ks
-template <bool KC>
+// per-lane byte offset within a half image of a fragment: 32x32x16 (F16 false) -- the 32-row
+// block at image row rb, k16-step ks; 16x16x32 (F16) -- the 16-row block at rb, k32-step ks
+template <bool KC, bool F16 = false>
 __device__ __forceinline__ unsigned frag_addr(int rb, int ks, int lane) {
-  if constexpr (KC) {
-    const int row = rb + (lane & 31);
-    const int pos = (2 * ks + (lane >> 5)) ^ ((row >> 1) & 7);
-    return (unsigned)(row * 128 + pos * 16);
+  if constexpr (F16) {
+    if constexpr (KC) {  // lane: row l&15, k chunk 4 ks + (l >> 4)
+      const int row = rb + (lane & 15);
+      const int pos = (4 * ks + (lane >> 4)) ^ ((row >> 1) & 7);
+      return (unsigned)(row * 128 + pos * 16);
+    } else {  // 16-lane group g: k rows 32 ks + 8 g + (0..3 | 4..7), lane 4q+p: row q, cols 4p..4p+3
+      const int i = lane & 15, q = i >> 2, pp = i & 3;
+      const int kk = 32 * ks + 8 * (lane >> 4) + q;
+      const int ro = rb + 4 * pp;
+      const int pos = (ro >> 3) ^ tr_swz(kk);
+      return (unsigned)(kk * 256 + pos * 16 + 2 * (ro & 4));
+    }
   } else {
-    const int i = lane & 15, q = i >> 2, pp = i & 3;
-    const int kk = 16 * ks + 8 * (lane >> 5) + q;
-    const int ro = rb + 16 * ((lane >> 4) & 1) + 4 * pp;
-    const int pos = (ro >> 3) ^ (4 * (kk & 3));
-    return (unsigned)(kk * 256 + pos * 16 + 2 * (ro & 4));
+    if constexpr (KC) {
+      const int row = rb + (lane & 31);
+      const int pos = (2 * ks + (lane >> 5)) ^ ((row >> 1) & 7);
+      return (unsigned)(row * 128 + pos * 16);
+    } else {
+      const int i = lane & 15, q = i >> 2, pp = i & 3;
+      const int kk = 16 * ks + 8 * (lane >> 5) + q;
+      const int ro = rb + 16 * ((lane >> 4) & 1) + 4 * pp;
+      const int pos = (ro >> 3) ^ tr_swz(kk);
+      return (unsigned)(kk * 256 + pos * 16 + 2 * (ro & 4));
+    }
   }
 }
 
@@ -151,44 +168,97 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
-// main-loop state of one workgroup (registers once inlined)
-template <bool AT, bool BT>
+// main-loop state of one workgroup (registers once inlined). ST: stamped diagnostics build --
+// per wave, the shader-clock cycles of each of a k-tile's 8 barrier-delimited slots summed over
+// the k-loop (mvae_bench_gemm with MVAE_STAMPS=2; never in the step)
+// F16: v_mfma_f32_16x16x32_bf16 (acc4: 8 x 4 blocks of 16x16 per wave) instead of 32x32x16 (acc:
+// 4 x 2 blocks of 32x32); the same cycles per FLOP, but the chip holds a higher clock on it on
+// random data (MI355X_MICROARCH.md, DVFS give-back item 7).
+template <bool AT, bool BT, bool ST = false, bool F16 = false>
 struct E8 {
   static constexpr bool KA = !AT, KB = BT;  // operand images k-contiguous?
-  HLoad<KA, 64> la;
-  HLoad<KB, 32> lb;
-  f32x16 acc[4][2];
-  bf16x8 fa[2][4], fb0[4], fb1[4];  // A-sub [block][k16-step], B-sub 0 / 1 [k16-step]
-  unsigned aA[KA ? 4 : 2], aB[KB ? 4 : 1];
+  HLoad<KA> la;
+  HLoad<KB> lb;
+  f32x16 acc[F16 ? 1 : 4][2];
+  f32x4 acc4[F16 ? 8 : 1][4];
+  // A-sub 0 / 1 (64 rows x 64 k) and B-sub 0 / 1 (32 cols x 64 k) fragments: 32x32x16 fa[4 r + ks]
+  // (r 0..1, k16-step ks 0..3), fb[ks]; 16x16x32 fa[4 ks + r] (k32-step ks 0..1, r 0..3),
+  // fb[2 ks + nb] (nb 0..1)
+  bf16x8 fa0[8], fa1[8], fb0[4], fb1[4];
+  // fragment base addresses: 32x32 A [ks] / [r], B [ks] / [-]; 16x16 A [ks] / [r], B [ks] / [nb]
+  unsigned aA[4], aB[4];
   const unsigned short* A;
   const unsigned short* Bm;
   short* smem;
   int wave;
+  unsigned long long st_last, st_acc[ST ? 8 : 1];
+
+  // the barrier closing slot K of a k-tile (stamped builds: its cycles since the previous one)
+  template <int K>
+  __device__ __forceinline__ void sbar() {
+    bar();
+    if constexpr (ST) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      st_acc[K] += t - st_last;
+      st_last = t;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
 
   // A half H of buffer Bf at byte (2 H + Bf) EHB; B half H at (4 + 2 H + Bf) EHB (aB includes 4 EHB)
   template <int H, int Bf>
-  __device__ __forceinline__ void rd_a() {
+  __device__ __forceinline__ void rd_a(bf16x8 (&fa)[8]) {
     constexpr int O = (2 * H + Bf) * EHB;
-    if constexpr (KA) {
+    if constexpr (F16) {
+      if constexpr (KA) {  // rows + 16 r: immediate; k32-step: base
+        fa[0] = rd_b128<O>(aA[0]);
+        fa[1] = rd_b128<O + 2048>(aA[0]);
+        fa[2] = rd_b128<O + 2 * 2048>(aA[0]);
+        fa[3] = rd_b128<O + 3 * 2048>(aA[0]);
+        fa[4] = rd_b128<O>(aA[1]);
+        fa[5] = rd_b128<O + 2048>(aA[1]);
+        fa[6] = rd_b128<O + 2 * 2048>(aA[1]);
+        fa[7] = rd_b128<O + 3 * 2048>(aA[1]);
+      } else {             // k32-step + 32 k-rows: immediate; row block: base
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          fa[r] = rd_tr<O>(aA[r]);
+          fa[4 + r] = rd_tr<O + 8192>(aA[r]);
+        }
+      }
+    } else if constexpr (KA) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        fa[0][ks] = rd_b128<O>(aA[ks]);
-        fa[1][ks] = rd_b128<O + 32 * 128>(aA[ks]);
+        fa[ks] = rd_b128<O>(aA[ks]);
+        fa[4 + ks] = rd_b128<O + 32 * 128>(aA[ks]);
       }
     } else {
 #pragma unroll
       for (int r = 0; r < 2; ++r) {
-        fa[r][0] = rd_tr<O>(aA[r]);
-        fa[r][1] = rd_tr<O + 4096>(aA[r]);
-        fa[r][2] = rd_tr<O + 2 * 4096>(aA[r]);
-        fa[r][3] = rd_tr<O + 3 * 4096>(aA[r]);
+        fa[4 * r] = rd_tr<O>(aA[r]);
+        fa[4 * r + 1] = rd_tr<O + 4096>(aA[r]);
+        fa[4 * r + 2] = rd_tr<O + 2 * 4096>(aA[r]);
+        fa[4 * r + 3] = rd_tr<O + 3 * 4096>(aA[r]);
       }
     }
   }
   template <int H, int Bf>
   __device__ __forceinline__ void rd_b(bf16x8 (&fb)[4]) {
     constexpr int O = (2 * H + Bf) * EHB;
-    if constexpr (KB) {
+    if constexpr (F16) {
+      if constexpr (KB) {
+        fb[0] = rd_b128<O>(aB[0]);
+        fb[1] = rd_b128<O + 2048>(aB[0]);
+        fb[2] = rd_b128<O>(aB[1]);
+        fb[3] = rd_b128<O + 2048>(aB[1]);
+      } else {
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          fb[nb] = rd_tr<O>(aB[nb]);
+          fb[2 + nb] = rd_tr<O + 8192>(aB[nb]);
+        }
+      }
+    } else if constexpr (KB) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) fb[ks] = rd_b128<O>(aB[ks]);
     } else {
@@ -198,17 +268,28 @@ struct E8 {
       fb[3] = rd_tr<O + 3 * 4096>(aB[0]);
     }
   }
-  // the quadrant's 8 MFMAs once this wave's reads have landed
+  // the quadrant's MFMAs (8 of 32x32x16 or 16 of 16x16x32) once this wave's reads have landed
   template <int M, int N>
-  __device__ __forceinline__ void mfma_q(const bf16x8 (&fb)[4]) {
+  __device__ __forceinline__ void mfma_q(const bf16x8 (&fa)[8], const bf16x8 (&fb)[4]) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (F16) {
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int r = 0; r < 2; ++r)
-        acc[2 * M + r][N] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[r][ks], fb[ks], acc[2 * M + r][N], 0, 0, 0);
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb)
+            acc4[4 * M + r][2 * N + nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                fa[4 * ks + r], fb[2 * ks + nb], acc4[4 * M + r][2 * N + nb], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+          acc[2 * M + r][N] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[4 * r + ks], fb[ks], acc[2 * M + r][N], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   }
@@ -222,84 +303,113 @@ struct E8 {
     const int pb = (pp.pab >> (4 * pr + 2)) & 3;
     lb.template issue<H>(Bm + pb * pp.pB, pp.g.ldb, t.ks + kt * EBK, t.ke, smem + (4 + 2 * H + Bf) * EH, wave);
   }
-  // k-tile `it` (its images in buffer Bf); (kt1, pr1), (kt2, pr2): (k-tile, pair) of it+1, it+2
+  // k-tile `it` (its images in buffer Bf); (kt1, pr1), (kt2, pr2): (k-tile, pair) of it+1, it+2.
+  // Fragment reads 4 / 4 / 8 / 8 per phase: B-sub 0 in q1, B-sub 1 in q2, A-sub 1 in q3 and the
+  // NEXT k-tile's A-sub 0 in q4 (its registers are free after q2), each waited for (vmcnt) in the
+  // phase before; the DMA of B1(it+1), A1(it+1), A0(it+2), B0(it+2) in q1..q4 refills a half
+  // >= 3 phases after its last read.
   template <int Bf>
   __device__ __forceinline__ void tile(const PParams& pp, const Tile& t, int it, int total, int kt1, int pr1,
                                        int kt2, int pr2) {
     constexpr int Bn = Bf ^ 1;
-    const bool m1 = it + 1 < total, m2 = it + 2 < total;
-    // q1: (0,0); B1(it) for q2 landed; B1(it+1)
-    rd_a<0, Bf>();
-    rd_b<0, Bf>(fb0);
+    // stamped builds' A/B switches (results meaningless): diag 1 = no DMA after the prologue,
+    // 64 = no fragment reads
+    const bool dma = !ST || !(pp.diag & 1), rdf = !ST || !(pp.diag & 64);
+    const bool n1 = it + 1 < total;  // a next k-tile exists (its A-sub 0 is read in q4)
+    const bool m1 = n1 && dma, m2 = it + 2 < total && dma;
+    // q1: (0,0) reads B0(it); B1(it) for q2 landed; B1(it+1)
+    if (rdf) rd_b<0, Bf>(fb0);
     wait_halves(m1 ? 3 : 1);
     if (m1) issue_b<1, Bn>(pp, t, kt1, pr1);
-    bar();
-    mfma_q<0, 0>(fb0);
-    bar();
-    // q2: (0,1); A1(it) for q3 landed; A1(it+1)
-    rd_b<1, Bf>(fb1);
+    sbar<0>();
+    mfma_q<0, 0>(fa0, fb0);
+    sbar<1>();
+    // q2: (0,1) reads B1(it); A1(it) for q3 landed; A1(it+1)
+    if (rdf) rd_b<1, Bf>(fb1);
     wait_halves(m1 ? 3 : 0);
     if (m1) issue_a<1, Bn>(pp, t, kt1, pr1);
-    bar();
-    mfma_q<0, 1>(fb1);
-    bar();
-    // q3: (1,1); A0(it+2) into the A0 half q1 read
-    rd_a<1, Bf>();
+    sbar<2>();
+    mfma_q<0, 1>(fa0, fb1);
+    sbar<3>();
+    // q3: (1,1) reads A1(it); A0(it+1) for q4 landed; A0(it+2) into the half A0(it) was read from
+    if (rdf) rd_a<1, Bf>(fa1);
+    if (m1) wait_halves(3);
     if (m2) issue_a<0, Bf>(pp, t, kt2, pr2);
-    bar();
-    mfma_q<1, 1>(fb1);
-    bar();
-    // q4: (1,0); A0(it+1), B0(it+1) for the next q1 landed; B0(it+2)
+    sbar<4>();
+    mfma_q<1, 1>(fa1, fb1);
+    sbar<5>();
+    // q4: (1,0) reads A0(it+1); B0(it+1) for the next q1 landed; B0(it+2)
+    if (rdf && n1) rd_a<0, Bn>(fa0);
     if (m1) wait_halves(m2 ? 3 : 2);
     if (m2) issue_b<0, Bf>(pp, t, kt2, pr2);
-    bar();
-    mfma_q<1, 0>(fb0);
-    bar();
+    sbar<6>();
+    mfma_q<1, 0>(fa1, fb0);
+    sbar<7>();
   }
 };
 
-template <bool AT, bool BT, int EPI, bool TE>
+template <bool AT, bool BT, int EPI, bool TE, bool ST = false, bool F16 = false>
 __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
   const Params& p = pp.g;
   if (epi_skip<EPI>(p.epi)) return;
   // [A0 b0 | A0 b1 | A1 b0 | A1 b1 | B0 b0 | B0 b1 | B1 b0 | B1 b1]; the row-major epilogue's two
   // 64-row bands and the BCE row partials reuse it after the k-loop
   constexpr int RING = 8 * EH;
-  constexpr int EPIL = TE ? 2 * (2 * 64 * 256 + 64 * 4 * 32) : 0;
+  constexpr int EPIL = 2 * (2 * 64 * 256 + 64 * 4 * 32);
   __shared__ __attribute__((aligned(16))) short smem[RING > EPIL ? RING : EPIL];
 
+  unsigned long long st_k0 = 0, st_k2 = 0;  // stamped builds: kernel start, k-loop end (realtime)
+  if constexpr (ST) st_k0 = __builtin_amdgcn_s_memrealtime();
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const Tile t = tile_of_t<256, 256>(p, true);
 
-  E8<AT, BT> s;
+  E8<AT, BT, ST, F16> s;
   s.A = pp.A + t.bi * p.sA;
   s.Bm = pp.B + t.bi * p.sB;
   s.smem = smem;
   s.wave = __builtin_amdgcn_readfirstlane(wave);
   s.la.init(p.lda, t.m0, p.M, wave, lane);
   s.lb.init(p.ldb, t.n0, p.N, wave, lane);
+  if constexpr (F16) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < 4; ++j) s.acc4[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  } else {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) s.acc[i][j][r] = 0.f;
-  constexpr bool KA = E8<AT, BT>::KA, KB = E8<AT, BT>::KB;
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s.acc[i][j][r] = 0.f;
+  }
+  constexpr bool KA = E8<AT, BT, ST, F16>::KA, KB = E8<AT, BT, ST, F16>::KB;
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
+  if constexpr (F16) {
 #pragma unroll
-  for (int i = 0; i < (KA ? 4 : 2); ++i)
-    s.aA[i] = lds0 + (KA ? frag_addr<true>(wm * 64, i, lane) : frag_addr<false>(wm * 64 + 32 * i, 0, lane));
+    for (int i = 0; i < 4; ++i) {
+      if (KA ? i < 2 : true)
+        s.aA[i] = lds0 + (KA ? frag_addr<true, true>(wm * 64, i, lane) : frag_addr<false, true>(wm * 64 + 16 * i, 0, lane));
+      if (i < 2)
+        s.aB[i] = lds0 + 4 * EHB + (KB ? frag_addr<true, true>(wn * 32, i, lane) : frag_addr<false, true>(wn * 32 + 16 * i, 0, lane));
+    }
+  } else {
 #pragma unroll
-  for (int i = 0; i < (KB ? 4 : 1); ++i)
-    s.aB[i] = lds0 + 4 * EHB + (KB ? frag_addr<true>(wn * 32, i, lane) : frag_addr<false>(wn * 32, 0, lane));
+    for (int i = 0; i < (KA ? 4 : 2); ++i)
+      s.aA[i] = lds0 + (KA ? frag_addr<true>(wm * 64, i, lane) : frag_addr<false>(wm * 64 + 32 * i, 0, lane));
+#pragma unroll
+    for (int i = 0; i < (KB ? 4 : 1); ++i)
+      s.aB[i] = lds0 + 4 * EHB + (KB ? frag_addr<true>(wn * 32, i, lane) : frag_addr<false>(wn * 32, 0, lane));
+  }
 
   const int np = (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
   const int nkt = t.ks < t.ke ? (t.ke - t.ks + EBK - 1) / EBK : 0;
   const int total = np * nkt;
   // waves 4-7 (the second half of every SIMD pair), as a scalar condition: s_barrier ignores EXEC
-  const bool lag = __builtin_amdgcn_readfirstlane(wave) >= 4;
+  // (stamped builds, diag 128: no stagger -- both halves in the same phase)
+  const bool lag = __builtin_amdgcn_readfirstlane(wave) >= 4 && !(ST && (pp.diag & 128));
 
   if (total > 0) {
     // (k-tile, pair) cursors of tiles it+1 and it+2
@@ -319,7 +429,15 @@ __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
     }
     wait_halves(total > 1 ? 4 : 2);
     bar();
+    s.template rd_a<0, 0>(s.fa0);  // tile 0's A-sub 0 (later tiles': read in the previous q4)
     if (lag) bar();
+    unsigned long long st_t0 = 0, st_r0 = 0;
+    if constexpr (ST) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s.st_acc[k] = 0;
+      st_r0 = __builtin_amdgcn_s_memrealtime();
+      st_t0 = s.st_last = __builtin_amdgcn_s_memtime();
+    }
     for (int it = 0; it < total; it += 2) {
       s.template tile<0>(pp, t, it, total, kt1, pr1, kt2, pr2);
       kt1 = kt2; pr1 = pr2; adv(kt2, pr2);
@@ -329,18 +447,77 @@ __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
       }
     }
     if (!lag) bar();
+    if constexpr (ST) {
+      const unsigned long long t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+      if (lane == 0) {
+        unsigned long long* o = pp.stamps + 16 * ((size_t)blockIdx.x * 8 + wave);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] = s.st_acc[k];
+        o[8] = t1 - st_t0; o[9] = r1 - st_r0; o[10] = total;
+        o[11] = st_r0 - st_k0;  // prologue (realtime ticks, 100 MHz)
+      }
+      st_k2 = r1;
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if constexpr (TE) epilogue_rm<EPI, 4, 2, 4, ENT>(p, t, s.acc, reinterpret_cast<float*>(smem), wm, wn, 0, nullptr,
-                                                   reinterpret_cast<float*>(smem) + 2 * 64 * 256);
-  else epilogue_g<EPI, 4, 2, 256, 4>(p, t, s.acc, reinterpret_cast<float*>(smem), wm, wn);
+  // The LDS row-major epilogue for every output (16-B global accesses when te, else element-wise).
+  // A wave's accumulator block (m, r) (A-sub m, 32-row block r) is tile rows 128 m + 64 wm + 32 r
+  // and its block n (B-sub n) tile columns 128 n + 32 wn (contiguous half images); band mi holds
+  // block (mi >> 1, mi & 1) of both wave rows (RMAP 1). The band's blocks are always the first
+  // ones (rotated down after each band: the band loop is not unrolled).
+  float* const lds_f = reinterpret_cast<float*>(smem);
+  if constexpr (F16) {  // 16x16 blocks: band mi = acc4[2 mi], acc4[2 mi + 1]; column block cb = 2 n + nb
+    auto wb = [&](float* band, int) {
+#pragma unroll
+      for (int rr = 0; rr < 2; ++rr)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            band[(wm * 32 + rr * 16 + 4 * (lane >> 4) + j) * 256 + (cb >> 1) * 128 + wn * 32 + (cb & 1) * 16 +
+                 (lane & 15)] = s.acc4[rr][cb][j];
+#pragma unroll
+      for (int i = 0; i + 2 < 8; ++i)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) s.acc4[i][cb] = s.acc4[i + 2][cb];
+    };
+    epilogue_rm_w<EPI, 4, 256, ENT, decltype(wb)&, 1>(p, t, wb, lds_f, 0, nullptr, lds_f + 2 * 64 * 256, TE);
+  } else {  // 32x32 blocks (C/D layout: col lane & 31, row (r & 3) + 8 (r >> 2) + 4 (lane >> 5))
+    auto wb = [&](float* band, int) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          band[(wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * 256 + n * 128 + wn * 32 + (lane & 31)] =
+              s.acc[0][n][r];
+#pragma unroll
+      for (int i = 0; i + 1 < 4; ++i)
+#pragma unroll
+        for (int n = 0; n < 2; ++n) s.acc[i][n] = s.acc[i + 1][n];
+    };
+    epilogue_rm_w<EPI, 4, 256, ENT, decltype(wb)&, 1>(p, t, wb, lds_f, 0, nullptr, lds_f + 2 * 64 * 256, TE);
+  }
+  if constexpr (ST) {  // epilogue: from the k-loop's end until every store of the workgroup issued
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (lane == 0 && st_k2) pp.stamps[16 * ((size_t)blockIdx.x * 8 + wave) + 12] = __builtin_amdgcn_s_memrealtime() - st_k2;
+  }
 }
 
 template <bool AT, bool BT, int EPI, bool TE>
 hipError_t launch_e(const PParams& p, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
-  hipLaunchKernelGGL((gemm_bf16e_kernel<AT, BT, EPI, TE>), dim3(nwg), dim3(ENT), 0, st, p);
+  const bool f16 = p.mf == 16;
+  if constexpr (EPI == EPI_STORE) {  // the stamped diagnostics builds (mvae_bench_gemm)
+    if (p.stamps) {
+      if (f16) hipLaunchKernelGGL((gemm_bf16e_kernel<AT, BT, EPI, TE, true, true>), dim3(nwg), dim3(ENT), 0, st, p);
+      else hipLaunchKernelGGL((gemm_bf16e_kernel<AT, BT, EPI, TE, true>), dim3(nwg), dim3(ENT), 0, st, p);
+      return hipGetLastError();
+    }
+  }
+  if (f16) hipLaunchKernelGGL((gemm_bf16e_kernel<AT, BT, EPI, TE, false, true>), dim3(nwg), dim3(ENT), 0, st, p);
+  else hipLaunchKernelGGL((gemm_bf16e_kernel<AT, BT, EPI, TE>), dim3(nwg), dim3(ENT), 0, st, p);
   return hipGetLastError();
 }
 

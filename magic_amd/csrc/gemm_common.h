@@ -39,6 +39,7 @@ struct PParams {
                                     // prologue (the k-loop multiplies stale LDS images)
   unsigned long long* stamps;       // stamped diagnostics builds (ST): 8 slots per workgroup
                                     // {start, prologue landed, k-loop done, end, stores issued}
+  int mf;                           // eight-phase kernel: MFMA shape 32 (32x32x16) or 16 (16x16x32)
 };
 
 // tanh as an odd [13/6] rational in x on [-7.905, 7.905] (clamped beyond, where tanh rounds to
@@ -344,12 +345,17 @@ __device__ __forceinline__ void st8_planes(unsigned short* cp, long long pc, int
 // buffers; nullptr: a 16-lane xor-shuffle tree per pass instead (its four dependent lane
 // exchanges behind each pass's transcendentals measured ~9 us per 256x256 tile,
 // tools/micro/epi.hip)
-template <int EPI, int MI, int NI, int NWN, int NTH>
-__device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x16 (&acc)[MI][NI],
-                                            float* lds, int wm, int wn, int diag = 0,
-                                            unsigned long long* issued = nullptr,
-                                            float* rpl = nullptr) {
-  constexpr int TW = NWN * NI * 32, BAND = 64 * TW;  // band row width, floats per band buffer
+// Generic form: write_band(band, mi) writes this wave's part of band mi (row-major, TW floats
+// per band row) from its accumulators in whatever MFMA layout they are; vec = false: every
+// global access element-wise (bases / strides not 16-B aligned, wide_epi_vec_ok false).
+// RMAP: tile row of band row br of band mi -- 0: wave row (br >> 5) owns rows [64 MI wr, +64 MI)
+// and band mi is its 32-row block mi; 1 (eight-phase kernel, MI 4): 32-row block mi of wave row
+// wr is tile rows 128 (mi >> 1) + 64 wr + 32 (mi & 1)
+template <int EPI, int MI, int TW, int NTH, class WB, int RMAP = 0>
+__device__ __forceinline__ void epilogue_rm_w(const Params& p, const Tile& t, WB&& write_band,
+                                              float* lds, int diag, unsigned long long* issued,
+                                              float* rpl, bool vec) {
+  constexpr int BAND = 64 * TW;  // floats per band buffer
   static_assert(TW % 128 == 0, "BCE row partials are per 128-column block");
   constexpr int CW = TW / 8;                    // 8-column chunks per band row
   constexpr int RP = NTH / CW;                  // band rows per reader pass
@@ -369,15 +375,16 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
   // each pass exposed one global-load latency per pass: 16 per 256-row tile). bf16 sources
   // stay packed (one uint4 per pass) until use.
   constexpr bool LD = is_dact<EPI> || BCE;
-  auto pass_row = [&](int mi, int q) {
-    const int br = rr + RP * q;                                          // band row
-    return t.m0 + (br >> 5) * (MI * 32) + mi * 32 + (br & 31);           // tile row -> global
+  auto tile_row = [&](int mi, int br) {
+    if constexpr (RMAP == 1) return (mi >> 1) * 128 + (br >> 5) * 64 + (mi & 1) * 32 + (br & 31);
+    return (br >> 5) * (MI * 32) + mi * 32 + (br & 31);
   };
+  auto pass_row = [&](int mi, int q) { return t.m0 + tile_row(mi, rr + RP * q); };  // band row -> global
   auto pass_nv = [&](int row) {
     return row >= p.M ? 0 : (col0 >= p.N ? 0 : (p.N - col0 < 8 ? p.N - col0 : 8));
   };
   // whole-chunk access of a partial last chunk (GemmEpi::padw)
-  auto pass_full = [&](int nv) { return nv == 8 || (e.padw && nv > 0); };
+  auto pass_full = [&](int nv) { return vec && (nv == 8 || (e.padw && nv > 0)); };
   constexpr bool bsrc = EPI == EPI_DACTB || EPI == EPI_BCEB;  // the operand is bf16
   // the operand rows of band mi's NQ passes: bf16 packed into sb (b16) or fp32 into sf
   auto load_band = [&](int mi, bool b16, float (&sf)[LD ? NQ : 1][8], uint4 (&sb)[LD ? NQ : 1]) {
@@ -427,19 +434,7 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
     } else {
       load_band(mi, false, sf, sb);
     }
-    // writer: this wave's 32 x (TW/4) block of the band, C/D layout -> row-major
-    if (!(diag & 4))
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        band[row * TW + wn * (NI * 32) + ni * 32 + (lane & 31)] = acc[0][ni][r];
-      }
-#pragma unroll
-    for (int j = 0; j + 1 < MI; ++j)
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) acc[j][ni] = acc[j + 1][ni];
+    if (!(diag & 4)) write_band(band, mi);
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < NQ; ++q) {
@@ -537,7 +532,7 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
       }
       if constexpr (BCE) {
         if (rpl) {
-          rpl[(br >> 5) * (MI * 32 * CW) + (mi * 32 + (br & 31)) * CW + c8] = rs;
+          rpl[tile_row(mi, br) * CW + c8] = rs;
         } else {
 #pragma unroll
           for (int off = 8; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
@@ -583,6 +578,32 @@ __device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x
     asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt) :: "memory");
     *issued = tt;
   }
+}
+
+// Row-major epilogue of the 32x32-MFMA kernels (waves 2 (M) x NWN (N), acc[MI][NI] of 32x32 blocks
+// in the C/D layout: col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)). The band's blocks
+// are always acc[0] (rotated down after each band: the band loop is not unrolled).
+template <int EPI, int MI, int NI, int NWN, int NTH>
+__device__ __forceinline__ void epilogue_rm(const Params& p, const Tile& t, f32x16 (&acc)[MI][NI],
+                                            float* lds, int wm, int wn, int diag = 0,
+                                            unsigned long long* issued = nullptr,
+                                            float* rpl = nullptr, bool vec = true) {
+  constexpr int TW = NWN * NI * 32;
+  const int lane = threadIdx.x & 63;
+  auto wb = [&](float* band, int) {
+#pragma unroll
+    for (int ni = 0; ni < NI; ++ni)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+        band[row * TW + wn * (NI * 32) + ni * 32 + (lane & 31)] = acc[0][ni][r];
+      }
+#pragma unroll
+    for (int j = 0; j + 1 < MI; ++j)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) acc[j][ni] = acc[j + 1][ni];
+  };
+  epilogue_rm_w<EPI, MI, TW, NTH>(p, t, wb, lds, diag, issued, rpl, vec);
 }
 
 // the 128x128-tile kernels: 4 waves in 2x2, each 2x2 accumulators

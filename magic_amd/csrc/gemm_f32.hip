@@ -366,7 +366,7 @@ int gemm_plan_split(const GemmDesc& d, size_t max_ws) {
 }
 
 size_t gemm_workspace_elems(const GemmDesc& d) {
-  const int s = gemm_plan_split(d, ~size_t(0));
+  const int s = d.split > 0 ? d.split : gemm_plan_split(d, ~size_t(0));
   return s > 1 ? (size_t)d.batch * s * d.M * d.N : 0;
 }
 
@@ -388,6 +388,7 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
   if (!d.valu && gemm_bf16_wide(d)) gemm_bf16_wide_plan(d, wsz, &split, &p.tn, &p.tm);
   else split = gemm_plan_split(d, wsz);
   if (d.split > 0) split = d.split;
+  if (split > 1 && (!ws || (size_t)d.batch * split * d.M * d.N > ws_elems)) return hipErrorInvalidValue;
   p.split = split;
   const int kb = d.prec == GEMM_F32 ? BK : 64;  // k-tile of the kernel that runs
   const int ktiles = (d.K + kb - 1) / kb;

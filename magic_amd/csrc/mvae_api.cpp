@@ -1468,7 +1468,9 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   d.variant = variant & 15;
   d.prec = (variant >> 4) & 15;  // 0 fp32, 1 bf16, 2 fp32-accurate bf16 split
   if (d.variant == 9) { d.valu = 1; d.prec = GEMM_F32; d.variant = 0; }  // the fp32 VALU kernel
-  d.diag = (variant >> 12) & 63; // kernel timing diagnostics (results meaningless; 32: A/B switch)
+  d.diag = (variant >> 12) & 255; // kernel timing diagnostics (results meaningless; 32: A/B switch)
+  // MVAE_BENCH_SPLIT (diagnostics): split-K forced (0 / unset: the planner's)
+  if (const char* sp = std::getenv("MVAE_BENCH_SPLIT"); sp && std::atoi(sp) > 0) d.split = std::atoi(sp);
   unsigned short* planes = nullptr;
   const int np = d.prec == GEMM_F32 ? 0 : (d.prec == GEMM_BF16 ? 1 : 3);
   hipError_t e = hipMalloc(&A, na * 4);
@@ -1577,6 +1579,49 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
                    "k-loop %.2f, epilogue %.2f us; start p50/p90/max %.2f/%.2f/%.2f; end p10/p50/max %.2f/%.2f/%.2f\n",
                    M, N, K, n, (hi - lo) * 0.01, seg[0] / n, seg[1] / n, seg[2] / n,
                    st0s[n / 2], st0s[n * 9 / 10], st0s[n - 1], ends[n / 10], ends[n / 2], ends[n - 1]);
+    }
+  }
+  // MVAE_STAMPS=2 (diagnostics): one more launch of the stamped eight-phase build (EPI_STORE,
+  // C/D epilogue): per wave the shader cycles of each of a k-tile's 8 barrier-delimited slots,
+  // summed over its k-loop; printed per k-tile for waves 0-3 and 4-7 (the half one barrier
+  // behind), with the in-kernel clock (shader cycles / 100 MHz realtime)
+  if (const char* sp = std::getenv("MVAE_STAMPS"); e == hipSuccess && sp && *sp == '2') {
+    const size_t nmax = 1 << 16;
+    unsigned long long* sb = nullptr;
+    e = hipMalloc(&sb, nmax * 8 * 16 * 8);
+    if (e == hipSuccess) e = hipMemsetAsync(sb, 0, nmax * 8 * 16 * 8, st);
+    GemmDesc ds = d;
+    ds.stamps = sb;
+    if (e == hipSuccess) e = gemm_run(ds, ws, ws_n, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    std::vector<unsigned long long> h(nmax * 8 * 16);
+    if (e == hipSuccess) e = hipMemcpy(h.data(), sb, h.size() * 8, hipMemcpyDeviceToHost);
+    if (sb) (void)hipFree(sb);
+    double slot[2][8] = {}, tot[2] = {}, tiles[2] = {}, cyc = 0, rt = 0, pro = 0, loop_us = 0, epi = 0;
+    int nw = 0;
+    for (size_t w = 0; w < nmax * 8 && e == hipSuccess; ++w) {
+      const unsigned long long* q = &h[16 * w];
+      if (!q[10]) continue;
+      const int half = (int)(w % 8) / 4;
+      for (int k = 0; k < 8; ++k) slot[half][k] += (double)q[k];
+      tot[half] += (double)q[8];
+      tiles[half] += (double)q[10];
+      cyc += (double)q[8];
+      rt += (double)q[9];
+      pro += (double)q[11] * 0.01;
+      loop_us += (double)q[9] * 0.01;
+      epi += (double)q[12] * 0.01;
+      ++nw;
+    }
+    if (nw) {
+      std::fprintf(stderr, "[e8stamps] M %d N %d K %d: %d waves, clock %.3f GHz, k-loop cycles per k-tile: "
+                   "waves0-3 %.0f, waves4-7 %.0f; per workgroup: prologue %.2f us, k-loop %.2f us, epilogue %.2f us\n",
+                   M, N, K, nw, cyc / rt * 0.1, tot[0] / tiles[0], tot[1] / tiles[1], pro / nw, loop_us / nw, epi / nw);
+      for (int hf = 0; hf < 2; ++hf) {
+        std::fprintf(stderr, "[e8stamps]   waves%s slots per k-tile:", hf ? "4-7" : "0-3");
+        for (int k = 0; k < 8; ++k) std::fprintf(stderr, " %.0f", slot[hf][k] / tiles[hf]);
+        std::fprintf(stderr, "\n");
+      }
     }
   }
   if (t0) (void)hipEventDestroy(t0);

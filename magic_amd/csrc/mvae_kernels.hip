@@ -626,11 +626,14 @@ __global__ void copy2d_kernel(const float* __restrict__ s, int lds, float* __res
 // (x,y) samples ((c*x - s*y) + x_off, (s*x + c*y) + y_off), NEAREST = roundf, zero fill;
 // per-example coefficients precomputed in fp32 on the host), concatenated per pixel as
 // (lock, rotated, key) and divided by 255 -> X [B, H*W*3]. No FMA contraction, so the
-// gather indices match the host restatement bit for bit.
+// gather indices match the host restatement bit for bit (hipcc contracts even the *_rn
+// intrinsics into FMAs unless contraction is off: a few pixels per batch then sampled a
+// neighbour; caught by tests/test_input_pipeline.py's grey-value tables).
 __global__ void make_batch_kernel(const unsigned char* __restrict__ locks,
                                   const unsigned char* __restrict__ keys, int H, int W,
                                   const int* __restrict__ idx, const float4* __restrict__ coef,
                                   float div, float* __restrict__ x) {
+#pragma clang fp contract(off)  // (the *_rn intrinsics do not prevent it: their bodies are outside)
   const int b = blockIdx.y;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   const int HW = H * W;
@@ -639,8 +642,8 @@ __global__ void make_batch_kernel(const unsigned char* __restrict__ locks,
   const float4 cf = coef[b];
   const int yy = p / W, xx = p - yy * W;
   const float fx = (float)xx, fy = (float)yy;
-  const float xin = __fadd_rn(__fsub_rn(__fmul_rn(cf.x, fx), __fmul_rn(cf.y, fy)), cf.z);
-  const float yin = __fadd_rn(__fadd_rn(__fmul_rn(cf.y, fx), __fmul_rn(cf.x, fy)), cf.w);
+  const float xin = (cf.x * fx - cf.y * fy) + cf.z;  // unfused: fp contract(off) above
+  const float yin = (cf.y * fx + cf.x * fy) + cf.w;
   const float xr = roundf(xin), yr = roundf(yin);
   const unsigned char* L = locks + (size_t)id * HW;
   float rot = 0.f;
@@ -663,6 +666,7 @@ __global__ __launch_bounds__(256) void make_batch4_kernel(const unsigned char* _
                                                           int W, const int* __restrict__ idx,
                                                           const float4* __restrict__ coef, float div,
                                                           float* __restrict__ x) {
+#pragma clang fp contract(off)  // as make_batch_kernel: the coordinates are unfused mul / add / sub
   __shared__ __attribute__((aligned(16))) float seg[3 * MB_PIX];
   const int b = blockIdx.y;
   const int tid = threadIdx.x;
@@ -682,8 +686,8 @@ __global__ __launch_bounds__(256) void make_batch4_kernel(const unsigned char* _
       const int p = p0 + j;
       const int yy = p / W, xx = p - yy * W;
       const float fx = (float)xx, fy = (float)yy;
-      const float xin = __fadd_rn(__fsub_rn(__fmul_rn(cf.x, fx), __fmul_rn(cf.y, fy)), cf.z);
-      const float yin = __fadd_rn(__fadd_rn(__fmul_rn(cf.y, fx), __fmul_rn(cf.x, fy)), cf.w);
+      const float xin = (cf.x * fx - cf.y * fy) + cf.z;  // unfused: fp contract(off) above
+      const float yin = (cf.y * fx + cf.x * fy) + cf.w;
       const float xr = roundf(xin), yr = roundf(yin);
       float rot = 0.f;
       if (xr >= 0.f && xr <= (float)(W - 1) && yr >= 0.f && yr <= (float)(H - 1))

@@ -33,7 +33,18 @@ def shapes(cfg):
         ("enc_bwd_w_h", e + 1, e, 2 * B, 1, 0, 2, 0),
         ("head_fwd", 3 * B, 2 * L, e + 1, 0, 0, 1, 0),
         ("head_bwd_d", 4 * B, e, 2 * L, 0, 1, 1, 2),
+        ("head_bwd_w", e + 1, 2 * L, 2 * B, 1, 0, 2, 0),
+        ("dec_fwd_1", B, cfg.dec[0], L + 1, 0, 0, 1, 1),
+        ("dec_bwd_w_1", L + 1, cfg.dec[0], B, 1, 0, 1, 0),
+        ("dec_bwd_d_z", B, L, cfg.dec[0], 0, 1, 1, 0),
+        ("dec_fwd_2", B, d1, cfg.dec[0] + 1, 0, 0, 1, 1),
+        ("dec_bwd_d_2", B, cfg.dec[0], d1, 0, 1, 1, 2),
+        ("dec_bwd_w_2", cfg.dec[0] + 1, d1, B, 1, 0, 1, 0),
         ("square4096", 4096, 4096, 4096, 0, 0, 1, 0),
+        # L2-resident probes of the k-loop's operand path: one tile re-run from a warm L2, and
+        # 64 tiles over 16 MB of operands
+        ("l2_one", 256, 256, 2048, 0, 0, 1, 0),
+        ("l2_64", 2048, 2048, 2048, 0, 0, 1, 0),
     ]
 
 
