@@ -660,11 +660,12 @@ hipError_t launch_var(const PParams& p, bool at, bool bt, int variant, hipStream
 bool gemm_bf16_wide(const GemmDesc& d) {
   if (d.prec == GEMM_F32) return false;
   // 10-12, 15: default-shape variants of the ring kernel (C/D epilogue, forced tile N, no
-  // eight-phase kernel); 3: the ring kernel, 13 / 14: the eight-phase kernel (5 / 6: with the
-  // 16x16x32 / 32x32x16 MFMA), on any shape
+  // eight-phase kernel); 3: the ring kernel, 6 / 13 / 14: the eight-phase kernel, on any shape
   const int v = (d.variant >= 10 && d.variant != 13 && d.variant != 14) ? 0 : d.variant;
   if (v == 1 || v == 2 || v == 4) return false;  // 128x128 register-staged variants
-  if (v != 3 && v != 5 && v != 6 && v != 13 && v != 14 && (d.M < 256 || d.N < 256)) return false;
+  // output dimensions >= 128 (the thin decoder / latent-head GEMMs of C3-C5: a 256-row ring
+  // tile ran them 1.6-1.7x faster than the 128x128 register-staged kernel, profiles/r4/README.md)
+  if (v != 3 && v != 6 && v != 13 && v != 14 && (d.M < 128 || d.N < 128)) return false;
   // one k-tile and under a CU's worth of 256x256 tiles (dec layer 1: K = L + 1; the head's
   // dgrad: K = 2L): epilogue-bound on few CUs, the 128x128 kernels spread it wider
   const long long t256 = (long long)((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
@@ -699,8 +700,13 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
     for (int j = 0; j < d.nB; ++j) np += i + j < T;
   if (d.dynA) np = (np + (d.nB < T ? d.nB : T)) / 2;  // A's residual planes often all zero
   const bool big = d.M >= 256 && d.N >= 256;
-  const bool force_e8 = d.variant == 13 || d.variant == 14 || d.variant == 5 || d.variant == 6;
-  const bool allow_e8 = force_e8 || (d.variant == 0 && big);
+  const bool force_e8 = d.variant == 13 || d.variant == 14 || d.variant == 6;
+  // the eight-phase kernel where it measured faster than the ring kernels (profiles/r4): enough
+  // 256x256 tiles to fill the chip, or a long k-loop over >= 32 tiles; its (k-tile, pair)
+  // iterations copy both operand images (the ring kernel reuses an unchanged image)
+  const long long t256 = (long long)((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
+  const bool e8_rule = big && t256 >= 32 && (t256 >= 256 || (long long)np * kt >= 64);
+  const bool allow_e8 = force_e8 || (d.variant == 0 && e8_rule);
   double best = 1e30;
   WidePlan pl;
   // 192-row ring tiles: k-contiguous A, epilogues other than the BCE head / sigmoid
@@ -711,12 +717,12 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
     const bool e8 = cand == 2;
     const int w = cand == 0 || cand == 3 ? 256 : cand == 1 || cand == 4 ? 128 : TN_E8;
     const int tmr = cand >= 3 ? 192 : 256;
-    if (e8 ? !allow_e8 : force_e8) continue;
+    if (e8 ? !allow_e8 : (force_e8 || allow_e8)) continue;
     if (cand >= 3 && !t192) continue;
     if ((d.tm == 192 && t192 && cand != 3 && cand != 4) || (d.tm == 256 && cand >= 3)) continue;
     if (d.variant == 11 && w != 128) continue;
     if (d.variant == 12 && w != 256) continue;
-    if (!e8 && !big && d.variant != 3 && d.variant < 10) continue;
+    if (!e8 && (d.M < 128 || d.N < 128) && d.variant != 3 && d.variant < 10) continue;
     const int tnn = e8 ? 256 : w;
     const long long tiles = (long long)((d.M + tmr - 1) / tmr) * ((d.N + tnn - 1) / tnn) * d.batch;
     // ring kernels, measured: 4096^3 at 1.06 PF/s = 1.94 us per 256x256 k-tile per CU; the
@@ -748,20 +754,9 @@ void gemm_bf16_wide_plan(const GemmDesc& d, size_t max_ws, int* split, int* tn, 
   *split = pl.split; *tn = pl.tn; *tm = pl.tm;
 }
 
-// MVAE_E8_MF (A/B): the eight-phase kernel's MFMA shape, 16 = v_mfma_f32_16x16x32_bf16,
-// otherwise 32x32x16
-static int e8_mf() {
-  static const int mf = [] {
-    const char* v = std::getenv("MVAE_E8_MF");
-    return v && std::atoi(v) == 16 ? 16 : 32;
-  }();
-  return mf;
-}
-
 hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, hipStream_t st) {
   PParams p;
   p.g = g;
-  p.mf = d.variant == 5 ? 16 : d.variant == 6 ? 32 : e8_mf();
   p.A = d.Ap; p.pA = d.pA;
   p.B = d.Bp; p.pB = d.pB;
   p.dyn = d.dynA;
@@ -780,8 +775,7 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   for (int i = 0; i < n; ++i) p.pab |= (p.pa[i] | p.pb[i] << 2) << (4 * i);
   if (gemm_bf16_wide(d)) {
     // tile N: the planner's (gemm_run), 256 for the diagnostic variants of the 256x256 forms
-    const bool q = d.variant == 0 || d.variant == 3 || d.variant == 5 || d.variant == 6 ||
-                   (d.variant >= 10 && d.variant <= 15);
+    const bool q = d.variant == 0 || d.variant == 3 || d.variant == 6 || (d.variant >= 10 && d.variant <= 15);
     p.g.tn = q && (g.tn == 128 || g.tn == TN_E8) ? g.tn : 256;
     p.g.tm = q && p.g.tn != TN_E8 && g.tm == 192 && !d.at ? 192 : 256;
     const int tm = p.g.tm, tn = p.g.tn == TN_E8 ? 256 : p.g.tn;

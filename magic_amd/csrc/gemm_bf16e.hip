@@ -36,7 +36,6 @@ using namespace gemm;
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef short s16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) short lds_short;
 
 constexpr int EBK = 64;          // k-tile
@@ -58,8 +57,8 @@ constexpr int ENT = 512;
 // Rows past the end of a k-contiguous operand are clamped (their outputs are not stored).
 constexpr unsigned OOB = 0x80000000u;  // >= the resource's num_records: loads zeros
 // chunk swizzle of a row-contiguous image's k-row k: the 4 (k & 3) term spreads the four k-rows
-// of one ds_read_b64_tr_b16 block, the 2 ((k >> 3) & 1) term the two 8-row-apart blocks a
-// 32-lane half of the 16x16x32 B-operand read takes in the same columns (both conflict-free)
+// of one ds_read_b64_tr_b16 block over the bank row (the 2 ((k >> 3) & 1) term, constant within a
+// 32-lane half, kept from the removed 16x16x32 form: conflict-free either way)
 __device__ __forceinline__ int tr_swz(int k) { return (4 * (k & 3)) ^ (2 * ((k >> 3) & 1)); }
 template <bool KC>
 struct HLoad {
@@ -91,16 +90,18 @@ struct HLoad {
   }
   // half H of the k-tile at k0 (tile k-range ends at kend) from the plane at g into img;
   // wave: the wave index as a scalar
-  template <int H>
+  // chunks J0 .. J1-1 of the lane (the half's 2 DMA instructions, or one of them)
+  template <int H, int J0 = 0, int J1 = 2>
   __device__ __forceinline__ void issue(const unsigned short* g, int ld, int k0, int kend, short* img,
-                                        int wave) const {
+                                        int wave, bool lin = false) const {
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<unsigned short*>(g), (short)0, (int)OOB, 0x00020000);
     const unsigned soff = KC ? 2u * (unsigned)k0 : 2u * (unsigned)k0 * (unsigned)ld;
     const int kl = k0 + EBK <= kend ? (1 << 30) : kend - k0;  // chunks at k >= kl read zeros
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const unsigned v = kc[j] < kl ? voff[j][H] : OOB;
+    for (int j = J0; j < J1; ++j) {
+      unsigned v = kc[j] < kl ? voff[j][H] : OOB;
+      if (lin) v = 16u * (threadIdx.x + 512u * j);  // diagnostics: linear source (wrong data)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
           rs, (__attribute__((address_space(3))) void*)(img + (j * 8 + wave) * 512), 16, v, soff, 0, 0);
     }
@@ -123,34 +124,20 @@ __device__ __forceinline__ bf16x8 rd_tr(unsigned a) {
   asm volatile("ds_read_b64_tr_b16 %0, %1 offset:%2" : "=v"(hi) : "v"(a), "i"(OFF + 4 * 256));
   return __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
 }
-// per-lane byte offset within a half image of a fragment: 32x32x16 (F16 false) -- the 32-row
-// block at image row rb, k16-step ks; 16x16x32 (F16) -- the 16-row block at rb, k32-step ks
-template <bool KC, bool F16 = false>
+// per-lane byte offset within a half image of the fragment of the 32-row block at image row rb,
+// k16-step ks
+template <bool KC>
 __device__ __forceinline__ unsigned frag_addr(int rb, int ks, int lane) {
-  if constexpr (F16) {
-    if constexpr (KC) {  // lane: row l&15, k chunk 4 ks + (l >> 4)
-      const int row = rb + (lane & 15);
-      const int pos = (4 * ks + (lane >> 4)) ^ ((row >> 1) & 7);
-      return (unsigned)(row * 128 + pos * 16);
-    } else {  // 16-lane group g: k rows 32 ks + 8 g + (0..3 | 4..7), lane 4q+p: row q, cols 4p..4p+3
-      const int i = lane & 15, q = i >> 2, pp = i & 3;
-      const int kk = 32 * ks + 8 * (lane >> 4) + q;
-      const int ro = rb + 4 * pp;
-      const int pos = (ro >> 3) ^ tr_swz(kk);
-      return (unsigned)(kk * 256 + pos * 16 + 2 * (ro & 4));
-    }
+  if constexpr (KC) {
+    const int row = rb + (lane & 31);
+    const int pos = (2 * ks + (lane >> 5)) ^ ((row >> 1) & 7);
+    return (unsigned)(row * 128 + pos * 16);
   } else {
-    if constexpr (KC) {
-      const int row = rb + (lane & 31);
-      const int pos = (2 * ks + (lane >> 5)) ^ ((row >> 1) & 7);
-      return (unsigned)(row * 128 + pos * 16);
-    } else {
-      const int i = lane & 15, q = i >> 2, pp = i & 3;
-      const int kk = 16 * ks + 8 * (lane >> 5) + q;
-      const int ro = rb + 16 * ((lane >> 4) & 1) + 4 * pp;
-      const int pos = (ro >> 3) ^ tr_swz(kk);
-      return (unsigned)(kk * 256 + pos * 16 + 2 * (ro & 4));
-    }
+    const int i = lane & 15, q = i >> 2, pp = i & 3;
+    const int kk = 16 * ks + 8 * (lane >> 5) + q;
+    const int ro = rb + 16 * ((lane >> 4) & 1) + 4 * pp;
+    const int pos = (ro >> 3) ^ tr_swz(kk);
+    return (unsigned)(kk * 256 + pos * 16 + 2 * (ro & 4));
   }
 }
 
@@ -171,21 +158,18 @@ __device__ __forceinline__ void bar() {
 // main-loop state of one workgroup (registers once inlined). ST: stamped diagnostics build --
 // per wave, the shader-clock cycles of each of a k-tile's 8 barrier-delimited slots summed over
 // the k-loop (mvae_bench_gemm with MVAE_STAMPS=2; never in the step)
-// F16: v_mfma_f32_16x16x32_bf16 (acc4: 8 x 4 blocks of 16x16 per wave) instead of 32x32x16 (acc:
-// 4 x 2 blocks of 32x32); the same cycles per FLOP, but the chip holds a higher clock on it on
-// random data (MI355X_MICROARCH.md, DVFS give-back item 7).
-template <bool AT, bool BT, bool ST = false, bool F16 = false>
+// (Measured and removed, profiles/r4/README.md: a 16x16x32-MFMA form -- higher clock, more
+// cycles, no faster -- and issuing the DMA between the MFMAs -- 25 % slower.)
+template <bool AT, bool BT, bool ST = false>
 struct E8 {
   static constexpr bool KA = !AT, KB = BT;  // operand images k-contiguous?
   HLoad<KA> la;
   HLoad<KB> lb;
-  f32x16 acc[F16 ? 1 : 4][2];
-  f32x4 acc4[F16 ? 8 : 1][4];
-  // A-sub 0 / 1 (64 rows x 64 k) and B-sub 0 / 1 (32 cols x 64 k) fragments: 32x32x16 fa[4 r + ks]
-  // (r 0..1, k16-step ks 0..3), fb[ks]; 16x16x32 fa[4 ks + r] (k32-step ks 0..1, r 0..3),
-  // fb[2 ks + nb] (nb 0..1)
+  f32x16 acc[4][2];
+  // A-sub 0 / 1 (64 rows x 64 k) and B-sub 0 / 1 (32 cols x 64 k) fragments: fa[4 r + ks]
+  // (32-row block r 0..1, k16-step ks 0..3), fb[ks]
   bf16x8 fa0[8], fa1[8], fb0[4], fb1[4];
-  // fragment base addresses: 32x32 A [ks] / [r], B [ks] / [-]; 16x16 A [ks] / [r], B [ks] / [nb]
+  // fragment base addresses: A [ks] (k-contiguous) / [r], B [ks] / [0]
   unsigned aA[4], aB[4];
   const unsigned short* A;
   const unsigned short* Bm;
@@ -209,24 +193,7 @@ struct E8 {
   template <int H, int Bf>
   __device__ __forceinline__ void rd_a(bf16x8 (&fa)[8]) {
     constexpr int O = (2 * H + Bf) * EHB;
-    if constexpr (F16) {
-      if constexpr (KA) {  // rows + 16 r: immediate; k32-step: base
-        fa[0] = rd_b128<O>(aA[0]);
-        fa[1] = rd_b128<O + 2048>(aA[0]);
-        fa[2] = rd_b128<O + 2 * 2048>(aA[0]);
-        fa[3] = rd_b128<O + 3 * 2048>(aA[0]);
-        fa[4] = rd_b128<O>(aA[1]);
-        fa[5] = rd_b128<O + 2048>(aA[1]);
-        fa[6] = rd_b128<O + 2 * 2048>(aA[1]);
-        fa[7] = rd_b128<O + 3 * 2048>(aA[1]);
-      } else {             // k32-step + 32 k-rows: immediate; row block: base
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          fa[r] = rd_tr<O>(aA[r]);
-          fa[4 + r] = rd_tr<O + 8192>(aA[r]);
-        }
-      }
-    } else if constexpr (KA) {
+    if constexpr (KA) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         fa[ks] = rd_b128<O>(aA[ks]);
@@ -245,20 +212,7 @@ struct E8 {
   template <int H, int Bf>
   __device__ __forceinline__ void rd_b(bf16x8 (&fb)[4]) {
     constexpr int O = (2 * H + Bf) * EHB;
-    if constexpr (F16) {
-      if constexpr (KB) {
-        fb[0] = rd_b128<O>(aB[0]);
-        fb[1] = rd_b128<O + 2048>(aB[0]);
-        fb[2] = rd_b128<O>(aB[1]);
-        fb[3] = rd_b128<O + 2048>(aB[1]);
-      } else {
-#pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
-          fb[nb] = rd_tr<O>(aB[nb]);
-          fb[2 + nb] = rd_tr<O + 8192>(aB[nb]);
-        }
-      }
-    } else if constexpr (KB) {
+    if constexpr (KB) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) fb[ks] = rd_b128<O>(aB[ks]);
     } else {
@@ -268,40 +222,31 @@ struct E8 {
       fb[3] = rd_tr<O + 3 * 4096>(aB[0]);
     }
   }
-  // the quadrant's MFMAs (8 of 32x32x16 or 16 of 16x16x32) once this wave's reads have landed
+  // the quadrant's 8 MFMAs once this wave's reads have landed
   template <int M, int N>
   __device__ __forceinline__ void mfma_q(const bf16x8 (&fa)[8], const bf16x8 (&fb)[4]) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
-    if constexpr (F16) {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
+    for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-          for (int nb = 0; nb < 2; ++nb)
-            acc4[4 * M + r][2 * N + nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-                fa[4 * ks + r], fb[2 * ks + nb], acc4[4 * M + r][2 * N + nb], 0, 0, 0);
-    } else {
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-          acc[2 * M + r][N] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[4 * r + ks], fb[ks], acc[2 * M + r][N], 0, 0, 0);
-    }
+      for (int r = 0; r < 2; ++r)
+        acc[2 * M + r][N] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[4 * r + ks], fb[ks], acc[2 * M + r][N], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   }
-  template <int H, int Bf>
+  template <int H, int Bf, int J0 = 0, int J1 = 2>
   __device__ __forceinline__ void issue_a(const PParams& pp, const Tile& t, int kt, int pr) {
     const int pa = (pp.pab >> (4 * pr)) & 3;
-    la.template issue<H>(A + pa * pp.pA, pp.g.lda, t.ks + kt * EBK, t.ke, smem + (2 * H + Bf) * EH, wave);
+    la.template issue<H, J0, J1>(A + pa * pp.pA, pp.g.lda, t.ks + kt * EBK, t.ke, smem + (2 * H + Bf) * EH, wave,
+                                 ST && (pp.diag & 2));
   }
-  template <int H, int Bf>
+  template <int H, int Bf, int J0 = 0, int J1 = 2>
   __device__ __forceinline__ void issue_b(const PParams& pp, const Tile& t, int kt, int pr) {
     const int pb = (pp.pab >> (4 * pr + 2)) & 3;
-    lb.template issue<H>(Bm + pb * pp.pB, pp.g.ldb, t.ks + kt * EBK, t.ke, smem + (4 + 2 * H + Bf) * EH, wave);
+    lb.template issue<H, J0, J1>(Bm + pb * pp.pB, pp.g.ldb, t.ks + kt * EBK, t.ke, smem + (4 + 2 * H + Bf) * EH, wave,
+                                 ST && (pp.diag & 2));
   }
   // k-tile `it` (its images in buffer Bf); (kt1, pr1), (kt2, pr2): (k-tile, pair) of it+1, it+2.
   // Fragment reads 4 / 4 / 8 / 8 per phase: B-sub 0 in q1, B-sub 1 in q2, A-sub 1 in q3 and the
@@ -313,7 +258,7 @@ struct E8 {
                                        int kt2, int pr2) {
     constexpr int Bn = Bf ^ 1;
     // stamped builds' A/B switches (results meaningless): diag 1 = no DMA after the prologue,
-    // 64 = no fragment reads
+    // 2 = linear DMA source addresses, 64 = no fragment reads
     const bool dma = !ST || !(pp.diag & 1), rdf = !ST || !(pp.diag & 64);
     const bool n1 = it + 1 < total;  // a next k-tile exists (its A-sub 0 is read in q4)
     const bool m1 = n1 && dma, m2 = it + 2 < total && dma;
@@ -348,7 +293,7 @@ struct E8 {
   }
 };
 
-template <bool AT, bool BT, int EPI, bool TE, bool ST = false, bool F16 = false>
+template <bool AT, bool BT, int EPI, bool TE, bool ST = false>
 __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
   const Params& p = pp.g;
   if (epi_skip<EPI>(p.epi)) return;
@@ -365,44 +310,27 @@ __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
   const int wm = wave >> 2, wn = wave & 3;
   const Tile t = tile_of_t<256, 256>(p, true);
 
-  E8<AT, BT, ST, F16> s;
+  E8<AT, BT, ST> s;
   s.A = pp.A + t.bi * p.sA;
   s.Bm = pp.B + t.bi * p.sB;
   s.smem = smem;
   s.wave = __builtin_amdgcn_readfirstlane(wave);
   s.la.init(p.lda, t.m0, p.M, wave, lane);
   s.lb.init(p.ldb, t.n0, p.N, wave, lane);
-  if constexpr (F16) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) s.acc4[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  } else {
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s.acc[i][j][r] = 0.f;
-  }
-  constexpr bool KA = E8<AT, BT, ST, F16>::KA, KB = E8<AT, BT, ST, F16>::KB;
+      for (int r = 0; r < 16; ++r) s.acc[i][j][r] = 0.f;
+  constexpr bool KA = E8<AT, BT, ST>::KA, KB = E8<AT, BT, ST>::KB;
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
-  if constexpr (F16) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (KA ? i < 2 : true)
-        s.aA[i] = lds0 + (KA ? frag_addr<true, true>(wm * 64, i, lane) : frag_addr<false, true>(wm * 64 + 16 * i, 0, lane));
-      if (i < 2)
-        s.aB[i] = lds0 + 4 * EHB + (KB ? frag_addr<true, true>(wn * 32, i, lane) : frag_addr<false, true>(wn * 32 + 16 * i, 0, lane));
-    }
-  } else {
+  for (int i = 0; i < (KA ? 4 : 2); ++i)
+    s.aA[i] = lds0 + (KA ? frag_addr<true>(wm * 64, i, lane) : frag_addr<false>(wm * 64 + 32 * i, 0, lane));
 #pragma unroll
-    for (int i = 0; i < (KA ? 4 : 2); ++i)
-      s.aA[i] = lds0 + (KA ? frag_addr<true>(wm * 64, i, lane) : frag_addr<false>(wm * 64 + 32 * i, 0, lane));
-#pragma unroll
-    for (int i = 0; i < (KB ? 4 : 1); ++i)
-      s.aB[i] = lds0 + 4 * EHB + (KB ? frag_addr<true>(wn * 32, i, lane) : frag_addr<false>(wn * 32, 0, lane));
-  }
+  for (int i = 0; i < (KB ? 4 : 1); ++i)
+    s.aB[i] = lds0 + 4 * EHB + (KB ? frag_addr<true>(wn * 32, i, lane) : frag_addr<false>(wn * 32, 0, lane));
 
   const int np = (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
   const int nkt = t.ks < t.ke ? (t.ke - t.ks + EBK - 1) / EBK : 0;
@@ -467,23 +395,7 @@ __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
   // block (mi >> 1, mi & 1) of both wave rows (RMAP 1). The band's blocks are always the first
   // ones (rotated down after each band: the band loop is not unrolled).
   float* const lds_f = reinterpret_cast<float*>(smem);
-  if constexpr (F16) {  // 16x16 blocks: band mi = acc4[2 mi], acc4[2 mi + 1]; column block cb = 2 n + nb
-    auto wb = [&](float* band, int) {
-#pragma unroll
-      for (int rr = 0; rr < 2; ++rr)
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb)
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            band[(wm * 32 + rr * 16 + 4 * (lane >> 4) + j) * 256 + (cb >> 1) * 128 + wn * 32 + (cb & 1) * 16 +
-                 (lane & 15)] = s.acc4[rr][cb][j];
-#pragma unroll
-      for (int i = 0; i + 2 < 8; ++i)
-#pragma unroll
-        for (int cb = 0; cb < 4; ++cb) s.acc4[i][cb] = s.acc4[i + 2][cb];
-    };
-    epilogue_rm_w<EPI, 4, 256, ENT, decltype(wb)&, 1>(p, t, wb, lds_f, 0, nullptr, lds_f + 2 * 64 * 256, TE);
-  } else {  // 32x32 blocks (C/D layout: col lane & 31, row (r & 3) + 8 (r >> 2) + 4 (lane >> 5))
+  {  // 32x32 blocks (C/D layout: col lane & 31, row (r & 3) + 8 (r >> 2) + 4 (lane >> 5))
     auto wb = [&](float* band, int) {
 #pragma unroll
       for (int n = 0; n < 2; ++n)
@@ -508,16 +420,13 @@ __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
 template <bool AT, bool BT, int EPI, bool TE>
 hipError_t launch_e(const PParams& p, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
-  const bool f16 = p.mf == 16;
-  if constexpr (EPI == EPI_STORE) {  // the stamped diagnostics builds (mvae_bench_gemm)
+  if constexpr (EPI == EPI_STORE) {  // the stamped diagnostics build (mvae_bench_gemm)
     if (p.stamps) {
-      if (f16) hipLaunchKernelGGL((gemm_bf16e_kernel<AT, BT, EPI, TE, true, true>), dim3(nwg), dim3(ENT), 0, st, p);
-      else hipLaunchKernelGGL((gemm_bf16e_kernel<AT, BT, EPI, TE, true>), dim3(nwg), dim3(ENT), 0, st, p);
+      hipLaunchKernelGGL((gemm_bf16e_kernel<AT, BT, EPI, TE, true>), dim3(nwg), dim3(ENT), 0, st, p);
       return hipGetLastError();
     }
   }
-  if (f16) hipLaunchKernelGGL((gemm_bf16e_kernel<AT, BT, EPI, TE, false, true>), dim3(nwg), dim3(ENT), 0, st, p);
-  else hipLaunchKernelGGL((gemm_bf16e_kernel<AT, BT, EPI, TE>), dim3(nwg), dim3(ENT), 0, st, p);
+  hipLaunchKernelGGL((gemm_bf16e_kernel<AT, BT, EPI, TE>), dim3(nwg), dim3(ENT), 0, st, p);
   return hipGetLastError();
 }
 

@@ -39,7 +39,6 @@ struct PParams {
                                     // prologue (the k-loop multiplies stale LDS images)
   unsigned long long* stamps;       // stamped diagnostics builds (ST): 8 slots per workgroup
                                     // {start, prologue landed, k-loop done, end, stores issued}
-  int mf;                           // eight-phase kernel: MFMA shape 32 (32x32x16) or 16 (16x16x32)
 };
 
 // tanh as an odd [13/6] rational in x on [-7.905, 7.905] (clamped beyond, where tanh rounds to
