@@ -705,13 +705,21 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
   // 256x256 tiles to fill the chip, or a long k-loop over >= 32 tiles; its (k-tile, pair)
   // iterations copy both operand images (the ring kernel reuses an unchanged image)
   const long long t256 = (long long)((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
-  const bool e8_rule = big && t256 >= 32 && (t256 >= 256 || (long long)np * kt >= 64);
-  const bool allow_e8 = force_e8 || (d.variant == 0 && e8_rule);
-  double best = 1e30;
-  WidePlan pl;
   // 192-row ring tiles: k-contiguous A, epilogues other than the BCE head / sigmoid
   const bool t192 = tm192_enabled() && !d.at && d.epi.mode != EPI_BCE && d.epi.mode != EPI_BCEB &&
                     d.epi.mode != EPI_SIGMOID;
+  const long long tl192 = (long long)((d.M + 191) / 192) * ((d.N + 255) / 256) * d.batch;
+  // ... except (in-step A/B, profiles/r4/README.md): single-product GEMMs where one round of
+  // 192-row ring tiles keeps >= 4/3 as many CUs busy (C3 layer-0 forward: 256 vs 192 workgroups,
+  // 0.255 vs 0.276 ms; hidden forward 31.7 vs 32.7 us), and the weight gradient over the exact
+  // pixel operand's plane pairs (f32x, dynA), whose one A image the ring kernel copies once per
+  // k-tile for all of them (C2 layer-0 weight gradient 0.438 vs 0.451 ms)
+  const bool ring_fills = t192 && np == 1 && tl192 <= 256 && 3 * tl192 >= 4 * t256;
+  const bool e8_rule = big && t256 >= 32 && (t256 >= 256 || (long long)np * kt >= 64) && !ring_fills &&
+                       !(d.dynA && d.at);
+  const bool allow_e8 = force_e8 || (d.variant == 0 && e8_rule);
+  double best = 1e30;
+  WidePlan pl;
   for (int cand = 0; cand < 5; ++cand) {
     // candidates: ring 256x256, 256x128, eight-phase 256x256, ring 192x256, 192x128
     const bool e8 = cand == 2;
@@ -762,12 +770,17 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   p.dyn = d.dynA;
   p.diag = d.diag;
   p.stamps = d.stamps;
-  // plane pairs (i, j), i + j < max(nA, nB); the pairs with i = 0 first
+  // plane pairs (i, j), i + j < max(nA, nB); the pairs with i = 0 first, j snaking (ascending for
+  // even i, descending for odd i): (0,0) (0,1) (0,2) (1,1) (1,0) (2,0), so consecutive pairs share
+  // the B plane at both A-plane changes and the ring kernel copies 3 A + 5 B images per k-tile
+  // instead of 3 + 6
   int n = 0;
   const int T = d.nA > d.nB ? d.nA : d.nB;
   for (int i = 0; i < d.nA; ++i)
-    for (int j = 0; j < d.nB; ++j)
+    for (int jj = 0; jj < d.nB; ++jj) {
+      const int j = (i & 1) ? d.nB - 1 - jj : jj;
       if (i + j < T) { p.pa[n] = (unsigned char)i; p.pb[n] = (unsigned char)j; ++n; }
+    }
   p.npairs = n;
   p.npairs0 = d.nB < T ? d.nB : T;  // pairs with i == 0
   if (!p.dyn) p.npairs0 = n;
