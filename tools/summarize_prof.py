@@ -2,7 +2,9 @@
 """Summarise a rocprofv3 --kernel-trace CSV: per (kernel, grid) dispatch group, the call
 count and mean/min/max duration, so templated GEMM launches of different shapes are
 distinguishable (rocprofv3 demangles without template arguments, so instantiations are told
-apart by Kernel_Id). Usage: summarize_prof.py <run_kernel_trace.csv> [--top N]"""
+apart by Kernel_Id). Usage: summarize_prof.py <run_kernel_trace.csv> [--top N] [--filter SUBSTR]
+(--filter: only kernels whose name contains SUBSTR, e.g. "mvae::" for the library's own kernels
+without the bench harness's torch kernels)"""
 import collections
 import csv
 import sys
@@ -11,7 +13,8 @@ import sys
 def main():
     path = sys.argv[1]
     top = int(sys.argv[sys.argv.index("--top") + 1]) if "--top" in sys.argv else 40
-    rows = list(csv.DictReader(open(path)))
+    flt = sys.argv[sys.argv.index("--filter") + 1] if "--filter" in sys.argv else ""
+    rows = [r for r in csv.DictReader(open(path)) if flt in r["Kernel_Name"]]
     g = collections.defaultdict(list)
     for r in rows:
         name = f'{r["Kernel_Name"]} #{r.get("Kernel_Id", "")}'
