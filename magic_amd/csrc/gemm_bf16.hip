@@ -711,9 +711,7 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
   const long long tl192 = (long long)((d.M + 191) / 192) * ((d.N + 255) / 256) * d.batch;
   // ... except (in-step A/B, profiles/r4/README.md) single-product GEMMs where one round of
   // 192-row ring tiles keeps >= 4/3 as many CUs busy (C3 layer-0 forward: 256 vs 192 workgroups,
-  // 0.255 vs 0.276 ms; hidden forward 31.7 vs 32.7 us). (The C2 layer-0 weight gradient stays on
-  // the eight-phase kernel: 0.451 ms in one 160-tile round without split-K slabs, against 0.438 ms
-  // for the ring kernel's split-K plan, which moves 783 MB of HBM traffic instead of ~0.45 GB.)
+  // 0.255 vs 0.276 ms; hidden forward 31.7 vs 32.7 us)
   const bool ring_fills = t192 && np == 1 && tl192 <= 256 && 3 * tl192 >= 4 * t256;
   const bool e8_rule = big && t256 >= 32 && (t256 >= 256 || (long long)np * kt >= 64) && !ring_fills;
   const bool allow_e8 = force_e8 || (d.variant == 0 && e8_rule);
