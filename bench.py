@@ -49,6 +49,8 @@ F32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (
 BF16_MFMA_PEAK_TFLOPS = 2500.0   # dense
 HBM_PEAK_GBS = 8000.0
 PMC_REGIONS_BW = ("deinterleave", "latent_bwd", "adam")
+# the layer-0 pair and the decoder-output trio: HBM traffic and the MFMA-busy fraction per region
+PMC_REGIONS_MFMA = ("enc_fwd_0", "enc_bwd_w_0", "dec_fwd_out_bce", "dec_bwd_d_out", "dec_bwd_w_out")
 
 
 def parse_args(argv=None):
@@ -734,12 +736,25 @@ def rooflines(args, m):
     if "dec_fwd_out_bce" in regions:
         ms_b = regions["dec_fwd_out_bce"][0] / args.region_steps
         by_b = 12.0 * cfg.D * cfg.batch
+        # what the fused kernel moves: the target (its bf16 plane for binary pixels, else fp32)
+        # and dU as the next GEMMs' planes (fp32 when they run native fp32); the logits never
+        # reach HBM. Its bound: max(MFMA time of the decoder-output product at the dense peak of
+        # the arithmetic it runs on, HBM time of those bytes at 8 TB/s)
+        np_b = 1 if cfg.precision == "bf16" else (6 if cfg.precision == "f32x" else 0)
+        by_f = cfg.D * cfg.batch * ((2.0 + 2.0 * (1 if np_b == 1 else 3)) if np_b else 8.0)
+        fl_b = region_flops(cfg, "dec_fwd_out_bce") * (np_b if np_b else 1)
+        t_mfma = fl_b / ((BF16_MFMA_PEAK_TFLOPS if np_b else F32_MFMA_PEAK_TFLOPS) * 1e12)
+        t_hbm = by_f / (HBM_PEAK_GBS * 1e9)
         loss_roofline["bce_head"] = {
             "bytes": by_b, "avg_ms": round(ms_b, 4),
             "gbs": round(by_b / (ms_b * 1e-3) / 1e9, 1),
             "frac": round(by_b / (ms_b * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "note": "BASELINE.md §4: 12*D B/pair (logits, targets, dlogits); fused into the "
-                    "decoder-output GEMM epilogue, whose time is MFMA-bound"}
+            "bytes_fused": by_f, "mfma_bound_ms": round(t_mfma * 1e3, 4),
+            "hbm_bound_ms": round(t_hbm * 1e3, 4),
+            "frac_of_bound": round(max(t_mfma, t_hbm) / (ms_b * 1e-3), 4),
+            "note": "BASELINE.md §4: 12*D B/pair (logits, targets, dlogits) for the unfused head; "
+                    "the fused decoder-output GEMM moves bytes_fused (target + dU planes) and is "
+                    "bounded by max(mfma_bound_ms, hbm_bound_ms); frac_of_bound = that / avg_ms"}
     return roofline, loss_roofline
 
 
@@ -860,14 +875,19 @@ def main():
                 rf, lr = rooflines(args, m)
                 # the config's own HBM traffic and MFMA-busy counters (same passes as the headline)
                 if rf and world == 1 and args.pmc == "auto" and not args.dry_run:
-                    want = [m["dom"]] + [k for k in PMC_REGIONS_BW if k in m["regions"]]
-                    tr, how = pmc_traffic(args, want, names_c, config=cid, mfma=(m["dom"],))
+                    mf = [m["dom"]] + [k for k in PMC_REGIONS_MFMA if k in m["regions"] and k != m["dom"]]
+                    want = mf + [k for k in PMC_REGIONS_BW if k in m["regions"]]
+                    tr, how = pmc_traffic(args, want, names_c, config=cid, mfma=tuple(mf))
                     rf["traffic_method"] = how
                     if tr and m["dom"] in tr:
                         rf["traffic"] = tr[m["dom"]].get("hbm_bytes")
                         rf["traffic_detail"] = tr[m["dom"]]
                         if "mfma_busy" in tr[m["dom"]]:
                             rf["mfma_busy"] = tr[m["dom"]]["mfma_busy"]
+                    if tr:
+                        rf["pmc_regions"] = {k: tr[k] for k in mf if k in tr}
+                        if "dec_fwd_out_bce" in tr and lr and "bce_head" in lr:
+                            lr["bce_head"]["traffic"] = tr["dec_fwd_out_bce"].get("hbm_bytes")
                     for k in PMC_REGIONS_BW:
                         if tr and k in tr and lr and k in lr and "hbm_bytes" in tr[k]:
                             lr[k]["traffic"] = tr[k]["hbm_bytes"]
@@ -889,8 +909,9 @@ def main():
             cpu = cpu_baseline(cfg, dev, args.cpu_seconds)
         if roofline and world == 1 and args.pmc == "auto" and not args.dry_run:
             names = eng.timing_names()
-            want = [head["dom"]] + [k for k in PMC_REGIONS_BW if k in head["regions"]]
-            tr, how = pmc_traffic(args, want, names, mfma=(head["dom"],))
+            mf = [head["dom"]] + [k for k in PMC_REGIONS_MFMA if k in head["regions"] and k != head["dom"]]
+            want = mf + [k for k in PMC_REGIONS_BW if k in head["regions"]]
+            tr, how = pmc_traffic(args, want, names, mfma=tuple(mf))
             roofline["traffic_method"] = how
             if tr:
                 if head["dom"] in tr:
@@ -898,6 +919,9 @@ def main():
                     roofline["traffic_detail"] = tr[head["dom"]]
                     if "mfma_busy" in tr[head["dom"]]:
                         roofline["mfma_busy"] = tr[head["dom"]]["mfma_busy"]
+                roofline["pmc_regions"] = {k: tr[k] for k in mf if k in tr}
+                if "dec_fwd_out_bce" in tr and "bce_head" in loss_roofline:
+                    loss_roofline["bce_head"]["traffic"] = tr["dec_fwd_out_bce"].get("hbm_bytes")
                 for k in PMC_REGIONS_BW:
                     if k in tr and k in loss_roofline:
                         loss_roofline[k]["traffic"] = tr[k]["hbm_bytes"]

@@ -767,6 +767,9 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   p.dyn = d.dynA;
   p.diag = d.diag;
   p.stamps = d.stamps;
+  // tile order (A/B): MVAE_TILE_GROUP=G walks bands of G m-tiles n by n
+  static const int tile_group = [] { const char* v = std::getenv("MVAE_TILE_GROUP"); return v ? std::atoi(v) : 0; }();
+  p.g.group = tile_group;
   // plane pairs (i, j), i + j < max(nA, nB); the pairs with i = 0 first, j snaking (ascending for
   // even i, descending for odd i): (0,0) (0,1) (0,2) (1,1) (1,0) (2,0), so consecutive pairs share
   // the B plane at both A-plane changes and the ring kernel copies 3 A + 5 B images per k-tile

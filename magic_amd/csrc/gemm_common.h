@@ -22,6 +22,8 @@ struct Params {
   int ntm, ntn;
   int tn;                   // bf16 DMA kernels: ring-kernel tile N (256 or 128) or TN_E8
   int tm = 256;             // ... and ring-kernel tile M (256, or 192 for a k-contiguous A)
+  int group = 0;            // tile order: 0 = row by row (n fastest); G > 0 = bands of G m-tiles
+                            // walked n by n, so an XCD's resident tiles share A and B in its L2
   GemmEpi epi;
 };
 constexpr int TN_E8 = 2;    // Params::tn of the 256 x 256 eight-phase kernel (gemm_bf16e.hip)
@@ -158,8 +160,16 @@ __device__ __forceinline__ Tile tile_of_t(const Params& p, bool remap) {
   const int b = remap ? xcd_remap(blockIdx.x, nwg) : (int)blockIdx.x;
   t.z = b / tiles;
   const int rem = b - t.z * tiles;
-  const int mt = rem / p.ntn;
-  t.nt = rem - mt * p.ntn;
+  int mt;
+  if (p.group > 0) {
+    const int band = rem / (p.group * p.ntn), m0 = band * p.group;
+    const int gsz = min(p.ntm - m0, p.group), r = rem - band * p.group * p.ntn;
+    t.nt = r / gsz;
+    mt = m0 + (r - t.nt * gsz);
+  } else {
+    mt = rem / p.ntn;
+    t.nt = rem - mt * p.ntn;
+  }
   t.bi = t.z / p.split;
   t.si = t.z - t.bi * p.split;
   t.m0 = mt * TBM;
