@@ -767,9 +767,11 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   p.dyn = d.dynA;
   p.diag = d.diag;
   p.stamps = d.stamps;
-  // tile order (A/B): MVAE_TILE_GROUP=G walks bands of G m-tiles n by n
-  static const int tile_group = [] { const char* v = std::getenv("MVAE_TILE_GROUP"); return v ? std::atoi(v) : 0; }();
-  p.g.group = tile_group;
+  // tile order: bands of 8 m-tiles walked n by n when a row has >= 8 n-tiles, so the 32 tiles
+  // an XCD holds at once share 8 A and 4 B tiles in its L2 (C5 latent-head forward
+  // 24576 x 4000 x 501: 0.177 -> 0.161 ms; neutral on the BCE head and the other shapes,
+  // profiles/r4/r4u_tile_group.txt); MVAE_TILE_GROUP=G overrides (A/B)
+  static const int tile_group = [] { const char* v = std::getenv("MVAE_TILE_GROUP"); return v ? std::atoi(v) : -1; }();
   // plane pairs (i, j), i + j < max(nA, nB); the pairs with i = 0 first, j snaking (ascending for
   // even i, descending for odd i): (0,0) (0,1) (0,2) (1,1) (1,0) (2,0), so consecutive pairs share
   // the B plane at both A-plane changes and the ring kernel copies 3 A + 5 B images per k-tile
@@ -794,6 +796,7 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
     const int tm = p.g.tm, tn = p.g.tn == TN_E8 ? 256 : p.g.tn;
     p.g.ntm = (d.M + tm - 1) / tm;
     p.g.ntn = (d.N + tn - 1) / tn;
+    p.g.group = tile_group >= 0 ? tile_group : (p.g.ntn >= 8 ? 8 : 0);
     switch (epi) {
       case EPI_STORE: return launch_wide<EPI_STORE>(p, d.at, d.bt, d.variant, st);
       case EPI_ACT: return launch_wide<EPI_ACT>(p, d.at, d.bt, d.variant, st);
