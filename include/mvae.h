@@ -165,7 +165,11 @@ int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* cou
  * side stream beside the dgrad chain, joined before the gradients they write are reported
  * final (mvae_backward / the end of each mvae_backward_part); "wgrad0_chunks" (1, 2, 4, 8;
  * default 1) splits the layer-0 weight gradient (40 MB of the 69 MB bucket at C4) into row
- * chunks that finish -- and can be all-reduced -- one after another. */
+ * chunks that finish -- and can be all-reduced -- one after another; "early_adam" (default 0)
+ * lets mvae_adam update the blocks after the layer-0 block on the side stream as soon as the
+ * backward has written their gradients (beside the layer-0 weight gradient): only for callers
+ * that do not modify MVAE_BUF_GRADS between mvae_backward and mvae_adam (no all-reduce);
+ * mvae_train_step uses it in the f32x mode. */
 int mvae_set_option(mvae_ctx* ctx, const char* name, int value);
 /* Both TF ApplyAdam updates from MVAE_BUF_GRADS (theta -= d1(g1) + d2(g2)).           */
 int mvae_adam(mvae_ctx* ctx, void* stream);

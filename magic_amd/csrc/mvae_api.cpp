@@ -93,6 +93,9 @@ struct mvae_ctx {
   size_t sync_next = 0;
   bool use_side = true;      // option "side_stream"
   bool side_pending = false; // side stream holds work the caller's stream has not joined
+  bool early_adam = false;   // option "early_adam": Adam of the parameters after the layer-0
+                             // block runs on the side stream beside the layer-0 weight gradient
+  bool early_fork = false;   // ... the side stream waits for the dgrad chain this step
   bool valu = true;          // skinny GEMMs on the fp32 VALU kernel (env MVAE_NO_VALU=1: off)
   std::vector<void*> allocs;
   // bf16 plane images (bf16 / f32x modes): fp32 buffer -> planes of the same layout
@@ -1126,6 +1129,14 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
         if ((rc = run(c, wg(i - 1), sd, wr(i - 1)))) return rc;
       }
     }
+    // early Adam: the side stream's Adam of the blocks after layer 0 (mvae_adam) may start once
+    // the dgrad chain -- the last reader of their weights -- is done, beside the layer-0
+    // weight gradient
+    c->early_fork = false;
+    if (c->early_adam && two) {
+      if ((rc = fork())) return rc;
+      c->early_fork = true;
+    }
     if ((rc = w0chunk(0))) return rc;
     if (R == 1 && (rc = tower())) return rc;
   } else if (part <= R) {
@@ -1167,6 +1178,13 @@ extern "C" int mvae_set_option(mvae_ctx* ctx, const char* name, int value) {
     if (ctx->side_pending)
       return fail(ctx, MVAE_ESTATE, "side_stream cannot change while side-stream work is pending");
     ctx->use_side = value != 0;
+    return MVAE_OK;
+  }
+  if (k == "early_adam") {
+    // only for callers that do not touch the gradients between mvae_backward and mvae_adam (no
+    // all-reduce): the side stream reads them as soon as the backward has written them
+    if (ctx->phase == 4) return fail(ctx, MVAE_ESTATE, "early_adam cannot change mid-backward");
+    ctx->early_adam = value != 0;
     return MVAE_OK;
   }
   if (k == "wgrad0_chunks") {
@@ -1225,7 +1243,21 @@ extern "C" int mvae_adam(mvae_ctx* ctx, void* stream) {
   a.lr2 = (c->cfg.lr[1] * std::sqrt(1.f - c->b2p[1])) / (1.f - c->b1p[1]);
   a.tp = planes_of(c, c->theta);
   hipStream_t st = (hipStream_t)stream;
-  {
+  if (c->early_fork && c->side) {
+    // the blocks after layer 0 on the side stream (already past the dgrad chain), layer 0 and the
+    // conv-tower blocks in front of it here; the caller's stream then waits for the side stream
+    c->early_fork = false;
+    const size_t l1 = c->nenc > 1 ? c->enc[1].off : c->head.off;
+    AdamArgs a1 = a, a0 = a;
+    a1.i0 = l1;
+    a0.i1 = l1;
+    MV_CHECK(launch_adam(a1, c->side));
+    {
+      TIMED("adam");
+      MV_CHECK(launch_adam(a0, st));
+    }
+    if (int rc = stream_wait(c, c->side, st)) return rc;
+  } else {
     TIMED("adam");
     MV_CHECK(launch_adam(a, st));
   }
@@ -1244,7 +1276,14 @@ extern "C" int mvae_train_step(mvae_ctx* ctx, const float* x, const float* areas
   hipStream_t st = (hipStream_t)stream;
   if (losses_out) MV_CHECK(hipMemcpyAsync(losses_out, ctx->losses, 5 * sizeof(float), hipMemcpyDeviceToDevice, st));
   if (dist_out) MV_CHECK(hipMemcpyAsync(dist_out, ctx->dist, ctx->B * sizeof(float), hipMemcpyDeviceToDevice, st));
-  if ((rc = mvae_backward(ctx, stream))) return rc;
+  // nothing touches the gradients between the two: Adam of the blocks after layer 0 may run
+  // beside the layer-0 weight gradient (option "early_adam"; measured faster in the f32x mode
+  // only, profiles/r4/r4ae_early_adam.txt)
+  const bool ea = ctx->early_adam;
+  ctx->early_adam = ea || ctx->np == 3;
+  rc = mvae_backward(ctx, stream);
+  ctx->early_adam = ea;
+  if (rc) return rc;
   return mvae_adam(ctx, stream);
 }
 

@@ -153,6 +153,7 @@ struct AdamArgs {
   float* theta; const float* g1; const float* g2; float* m1; float* v1; float* m2; float* v2;
   size_t n_all, n_enc; float lr1, lr2, b1, b2, eps;
   Planes tp;  // bf16 plane image of theta refreshed in the same pass (bf16 / f32x modes)
+  size_t i0 = 0, i1 = ~size_t(0);  // the index range [i0, min(i1, n_all)) this launch updates
 };
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
 hipError_t launch_split_planes(const float* src, size_t n, const Planes& dst, hipStream_t st);

@@ -637,8 +637,8 @@ __global__ void latent_bwd_kernel(const float* __restrict__ ms, EpsSrc es,
 // both from the pre-step gradients: theta = (theta - d1) - d2.  lr_t precomputed on the
 // host in fp32 exactly as TF ApplyAdam (lr*sqrt(1-b2^t)/(1-b1^t) with fp32 beta powers).
 __global__ void adam_kernel(AdamArgs a) {
-  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n_all) return;
+  const size_t i = a.i0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.i1) return;
   float th = a.theta[i];
   {
     const float g = a.g1[i];
@@ -878,7 +878,10 @@ hipError_t launch_latent_bwd(const float* ms, const LatentEps& le, const float* 
 }
 
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL(adam_kernel, dim3(nblocks(a.n_all, 256)), dim3(256), 0, st, a);
+  AdamArgs r = a;
+  r.i1 = a.i1 < a.n_all ? a.i1 : a.n_all;
+  if (r.i0 >= r.i1) return hipSuccess;
+  hipLaunchKernelGGL(adam_kernel, dim3(nblocks(r.i1 - r.i0, 256)), dim3(256), 0, st, r);
   return hipGetLastError();
 }
 

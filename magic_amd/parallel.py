@@ -28,6 +28,8 @@ split-K, so those rows are not bitwise equal to a single-process one-GEMM backwa
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -60,6 +62,15 @@ class DataParallelStep:
             # all-reduced while the next computes, instead of one transfer after the last GEMM
             engine.set_option("wgrad0_chunks", wgrad0_chunks)
             self._chunks_set = True
+        self._early_set = False
+        early = os.environ.get("MVAE_NO_EARLY_ADAM") != "1" and engine.cfg.precision == "f32x"
+        if not self.coll and hasattr(engine, "set_option") and early:
+            # no collective between backward() and adam(): Adam of the blocks after layer 0 runs
+            # on the engine's side stream beside the layer-0 weight gradient. Measured per mode
+            # (profiles/r4/r4ae_early_adam.txt): C2 (f32x) 2.775 -> 2.742 ms, C3 (bf16) 1.992 ->
+            # 2.005 ms, so f32x only; MVAE_NO_EARLY_ADAM=1: one Adam launch after the backward
+            engine.set_option("early_adam", 1)
+            self._early_set = True
         if hasattr(engine, "set_shard"):
             # the internal eps sampler draws this rank's rows of the global batch's stream,
             # so a sharded step without explicit eps equals the single-process step too
@@ -74,6 +85,9 @@ class DataParallelStep:
         if self._chunks_set:
             self.e.set_option("wgrad0_chunks", 1)
             self._chunks_set = False
+        if self._early_set:
+            self.e.set_option("early_adam", 0)
+            self._early_set = False
 
     def step(self, x, areas, eps=None):
         e = self.e

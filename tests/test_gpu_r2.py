@@ -306,6 +306,39 @@ def test_side_stream_schedule_is_bitwise_identical(prec):
 
 
 # ------------------------------------------------------------------ fp32 VALU kernel (skinny GEMMs)
+
+@pytest.mark.parametrize("prec", ["f32x", "bf16"])
+def test_early_adam_is_bitwise_identical(prec):
+    """Option early_adam (Adam of the blocks after layer 0 on the side stream, beside the layer-0
+    weight gradient) vs one Adam launch after the backward, and mvae_train_step (which uses it
+    in the f32x mode): bitwise identical parameters after three steps."""
+    cfg = preset("8c", image_size=40, batch=768, precision=prec).replace(enc=(400, 300, 260))
+    P = make_params(cfg)
+    X, areas, eps = make_inputs(cfg, cfg.batch)
+    x, a, e = to_dev(X), to_dev(areas), to_dev(eps)
+    outs = []
+    for mode in ("early", "late", "train_step"):
+        eng = _engine(cfg)  # fresh Adam state per mode
+        try:
+            eng.set_option("early_adam", 1 if mode == "early" else 0)
+            eng.load_params(P)
+            for _ in range(3):
+                if mode == "train_step":
+                    eng.train_step(x, a, e)
+                else:
+                    eng.forward(x, e)
+                    eng.metric(a)
+                    eng.backward()
+                    eng.adam()
+            torch.cuda.synchronize()
+            outs.append({k: v.cpu().numpy() for k, v in eng.params().items()})
+        finally:
+            eng.close()
+    for o in outs[1:]:
+        for k in outs[0]:
+            np.testing.assert_array_equal(outs[0][k], o[k])
+
+
 @pytest.mark.parametrize("at,bt", [(0, 0), (1, 0), (0, 1), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(1, 1, 1), (37, 53, 29), (12288, 40, 501), (21, 500, 4096),
                                    (4096, 20, 500), (16384, 500, 40), (501, 40, 8192), (70, 130, 65)])
