@@ -169,7 +169,9 @@ int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* cou
  * lets mvae_adam update the blocks after the layer-0 block on the side stream as soon as the
  * backward has written their gradients (beside the layer-0 weight gradient): only for callers
  * that do not modify MVAE_BUF_GRADS between mvae_backward and mvae_adam (no all-reduce);
- * mvae_train_step uses it in the f32x mode. */
+ * mvae_train_step uses it in the f32x mode; "bce_split" (default 1) runs a BCE head whose
+ * 256x256 tiles leave a partial last round as the whole rounds plus 256x128 tiles for the rest
+ * (the same results). */
 int mvae_set_option(mvae_ctx* ctx, const char* name, int value);
 /* Both TF ApplyAdam updates from MVAE_BUF_GRADS (theta -= d1(g1) + d2(g2)).           */
 int mvae_adam(mvae_ctx* ctx, void* stream);

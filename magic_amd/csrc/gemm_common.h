@@ -295,7 +295,7 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
         float s_ = 0.f;
 #pragma unroll
         for (int w = 0; w < WPB; ++w) s_ += red[(b * WPB + w) * TBM + r];
-        e.rowpart[(size_t)(t.m0 + r) * nblk + gb] = -s_;
+        e.rowpart[(size_t)(t.m0 + r) * (e.rp_ld ? e.rp_ld : nblk) + gb + e.rp_off] = -s_;
       }
     }
   }
@@ -545,7 +545,7 @@ __device__ __forceinline__ void epilogue_rm_w(const Params& p, const Tile& t, WB
         } else {
 #pragma unroll
           for (int off = 8; off >= 1; off >>= 1) rs += __shfl_xor(rs, off, 64);
-          if ((c8 & 15) == 0 && rok && gb < nblk) e.rowpart[(size_t)row * nblk + gb] = -rs;
+          if ((c8 & 15) == 0 && rok && gb < nblk) e.rowpart[(size_t)row * (e.rp_ld ? e.rp_ld : nblk) + gb + e.rp_off] = -rs;
         }
       }
     }
@@ -578,7 +578,7 @@ __device__ __forceinline__ void epilogue_rm_w(const Params& p, const Tile& t, WB
 #pragma unroll
         for (int j = 0; j < 4; ++j) t4[j] = t8[j] + t8[j + 4];
         const float sum = (t4[0] + t4[2]) + (t4[1] + t4[3]);
-        if (row < p.M && gbb < nblk) e.rowpart[(size_t)row * nblk + gbb] = -sum;
+        if (row < p.M && gbb < nblk) e.rowpart[(size_t)row * (e.rp_ld ? e.rp_ld : nblk) + gbb + e.rp_off] = -sum;
       }
     }
   }

@@ -108,6 +108,9 @@ struct mvae_ctx {
   // schedule (each GEMM tagged with its timing region)
   std::vector<GemmDesc> fwd_enc;  // encoder layers + head
   GemmDesc f_d1, f_d2, f_out;
+  GemmDesc f_out_a, f_out_b;  // f_out as whole rounds of 256x256 tiles + the rest (f_split)
+  bool f_split = false;
+  bool use_split = true;      // option "bce_split" (default 1)
   std::vector<GemmDesc> bwd_dec;  // W_out, D_out, W_d2, D_d2, W_d1, D_d1
   std::vector<GemmDesc> bwd_enc;  // W_head, D_head, (W_i, D_i)..., W_0
   std::vector<int> fwd_enc_r, bwd_dec_r, bwd_enc_r;
@@ -715,6 +718,37 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
       c->w0m[R].push_back(w.M);
     }
   }
+  {  // The BCE head in whole rounds: when its 256x256 tiles leave a partial last round on the
+     // 256 CUs (C2: 16 x 40 = 640 tiles = 2.5 rounds), the columns of the whole rounds run as one
+     // launch and the rest as 256x128 ring tiles (half the work per tile, so the last round takes
+     // about half as long); elementwise the same results and the same 128-column row partials.
+     // MVAE_BCE_SPLIT=0: never; option "bce_split" 0: one launch (A/B, tests)
+    static const bool on = [] { const char* v = std::getenv("MVAE_BCE_SPLIT"); return !(v && *v == '0'); }();
+    const GemmDesc& f = c->f_out;
+    const long long tm = (f.M + 255) / 256, tn = (f.N + 255) / 256, tiles = tm * tn;
+    const long long n1 = (tiles / 256) * 256 / tm;  // n-tiles of the whole rounds
+    c->f_split = false;
+    if (on && f.prec != GEMM_F32 && !f.valu && gemm_bf16_wide(f) && tiles > 256 && tiles % 256 != 0 &&
+        tiles % 256 <= 128 && n1 >= 1 && n1 < tn) {
+      const int c0 = (int)(256 * n1);
+      GemmDesc a = f, b = f;
+      a.N = c0;
+      a.epi.rp_ld = gemm_bce_nblk(f.N);
+      b.N = f.N - c0;
+      b.B = f.B + c0;
+      if (b.Bp) b.Bp = f.Bp + c0;
+      if (b.C) b.C = f.C + c0;
+      if (b.epi.cp) b.epi.cp = f.epi.cp + c0;
+      if (b.epi.x) b.epi.x = f.epi.x + c0;
+      if (b.epi.xp) b.epi.xp = f.epi.xp + c0;
+      b.epi.rp_ld = gemm_bce_nblk(f.N);
+      b.epi.rp_off = c0 / 128;
+      b.variant = 11;  // the ring kernel at 256x128 tiles
+      c->f_out_a = a;
+      c->f_out_b = b;
+      c->f_split = true;
+    }
+  }
   size_t ws = 0;
   auto wsz = [&](const GemmDesc& d) { ws = std::max(ws, gemm_workspace_elems(d)); };
   for (int R : {2, 4, 8})
@@ -1007,7 +1041,12 @@ extern "C" int mvae_forward(mvae_ctx* ctx, const float* x, const float* eps, voi
   if (rc) return rc;
   if ((rc = run(ctx, ctx->f_d1, st, ctx->f_d1_r))) return rc;
   if ((rc = run(ctx, ctx->f_d2, st, ctx->f_d2_r))) return rc;
-  if ((rc = run(ctx, ctx->f_out, st, ctx->f_out_r))) return rc;
+  if (ctx->f_split && ctx->use_split) {
+    if ((rc = run(ctx, ctx->f_out_a, st, ctx->f_out_r))) return rc;
+    if ((rc = run(ctx, ctx->f_out_b, st, ctx->f_out_r))) return rc;
+  } else if ((rc = run(ctx, ctx->f_out, st, ctx->f_out_r))) {
+    return rc;
+  }
   ctx->phase = 1;
   return MVAE_OK;
 }
@@ -1178,6 +1217,10 @@ extern "C" int mvae_set_option(mvae_ctx* ctx, const char* name, int value) {
     if (ctx->side_pending)
       return fail(ctx, MVAE_ESTATE, "side_stream cannot change while side-stream work is pending");
     ctx->use_side = value != 0;
+    return MVAE_OK;
+  }
+  if (k == "bce_split") {
+    ctx->use_split = value != 0;
     return MVAE_OK;
   }
   if (k == "early_adam") {

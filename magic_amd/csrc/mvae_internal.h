@@ -47,6 +47,8 @@ struct GemmEpi {
   float* y = nullptr;           // BCE: optional sigmoid output
   int ldy = 0;
   float* rowpart = nullptr;     // BCE: [M][nblk_n] per-row partial sums of the BCE terms
+  int rp_ld = 0, rp_off = 0;    // ... its row stride (0: this GEMM's nblk_n) and first block (a
+                                // launch over a column range of a wider head)
   // bf16 planes of the output (same layout/ld as C, plane stride pc): the operand image
   // of the next GEMM in the bf16 / f32x modes. ncp = 0 (none), 1 (RN) or 3 (exact split).
   unsigned short* cp = nullptr;

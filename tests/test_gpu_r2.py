@@ -339,6 +339,30 @@ def test_early_adam_is_bitwise_identical(prec):
             np.testing.assert_array_equal(outs[0][k], o[k])
 
 
+
+@pytest.mark.parametrize("prec", ["f32x", "bf16"])
+def test_bce_split_is_bitwise_identical(prec):
+    """The BCE head in whole rounds plus 256x128 ring tiles for the remaining columns (option
+    bce_split; 66 x 66 images, B = 4096: 16 x 18 = 288 tiles of 256x256 -> 16 n-tiles + 272
+    columns) vs one launch: bitwise identical losses, distance and gradients."""
+    cfg = preset("8c", image_size=66, batch=4096, precision=prec).replace(enc=(300, 260))
+    P = make_params(cfg)
+    X, areas, eps = make_inputs(cfg, cfg.batch)
+    eng = _engine(cfg)
+    try:
+        outs = []
+        for split in (1, 0):
+            eng.set_option("bce_split", split)
+            eng.load_params(P)
+            outs.append(gpu_phases(eng, X, areas, eps))
+        for u, v in zip(outs[0][:2], outs[1][:2]):
+            np.testing.assert_array_equal(u, v)
+        for d in (2, 3):
+            for k in outs[0][d]:
+                np.testing.assert_array_equal(outs[0][d][k], outs[1][d][k])
+    finally:
+        eng.close()
+
 @pytest.mark.parametrize("at,bt", [(0, 0), (1, 0), (0, 1), (1, 1)])
 @pytest.mark.parametrize("M,N,K", [(1, 1, 1), (37, 53, 29), (12288, 40, 501), (21, 500, 4096),
                                    (4096, 20, 500), (16384, 500, 40), (501, 40, 8192), (70, 130, 65)])
