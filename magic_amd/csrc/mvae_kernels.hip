@@ -392,7 +392,9 @@ __global__ void latent_fwd_kernel(const float* __restrict__ ms, EpsSrc es, float
 // the ordered sum over chunks. (With 128-row chunks every thread waited out 32 dependent
 // global loads in a row and the final pass another nchunk: 20-30 us per statistic for a few
 // hundred KB.)
-constexpr int CS_ROWS = 32;
+// 128-row chunks: 32-row ones left the final pass 256 dependent partials per column at C3
+// (colsq + coldot 36.5 -> 23.6 us, profiles/r4/r4aj_colstats.txt)
+constexpr int CS_ROWS = 128;
 constexpr int CS_PER = CS_ROWS / 4;  // rows per thread
 
 __global__ void colstats_part_kernel(int mode, const float* __restrict__ z, int B, int L, int ldz,
