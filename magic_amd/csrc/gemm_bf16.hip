@@ -712,7 +712,9 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
   // ... except (in-step A/B, profiles/r4/README.md) single-product GEMMs where one round of
   // 192-row ring tiles keeps >= 4/3 as many CUs busy (C3 layer-0 forward: 256 vs 192 workgroups,
   // 0.255 vs 0.276 ms; hidden forward 31.7 vs 32.7 us)
-  const bool ring_fills = t192 && np == 1 && tl192 <= 256 && 3 * tl192 >= 4 * t256;
+  // (a real one-round fill: not a tile count split-K multiplies anyway -- the C3 decoder-output
+  // dgrad, 86 vs 64 tiles, stays on the eight-phase kernel: 0.107 vs 0.115 ms in r4n)
+  const bool ring_fills = t192 && np == 1 && tl192 > 128 && tl192 <= 256 && 3 * tl192 >= 4 * t256;
   const bool e8_rule = big && t256 >= 32 && (t256 >= 256 || (long long)np * kt >= 64) && !ring_fills;
   const bool allow_e8 = force_e8 || (d.variant == 0 && e8_rule);
   double best = 1e30;
