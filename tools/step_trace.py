@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """One training step's kernel sequence from a rocprofv3 kernel trace of bench.py: the library's
-kernels (mvae::) between two Adam launches, for the step whose kernels overlap least (the
-bench's region pass serialises them on one stream), with start offsets, durations and the gap
-before each launch.  usage: python tools/step_trace.py <kernel_trace.csv>"""
+kernels (mvae::) from one de-interleave launch (the start of a step) to the next, for the step
+whose kernels overlap least (the bench's region pass serialises them on one stream), with start
+offsets, durations and the gap before each launch.  usage: python tools/step_trace.py <csv>"""
 import csv
 import re
 import sys
@@ -11,10 +11,10 @@ import sys
 def main():
     rows = [r for r in csv.DictReader(open(sys.argv[1])) if "mvae::" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    ad = [i for i, r in enumerate(rows) if "adam_kernel" in r["Kernel_Name"]]
+    ad = [i for i, r in enumerate(rows) if "deinterleave" in r["Kernel_Name"]]
     best = None
     for k in range(1, len(ad)):
-        seg = rows[ad[k - 1] + 1:ad[k] + 1]
+        seg = rows[ad[k - 1]:ad[k]]
         ov, last = 0, 0
         for r in seg:
             s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
