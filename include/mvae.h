@@ -111,7 +111,9 @@ enum {
   MVAE_BUF_DYN = 10      /* int32[1] (count 1): nonzero when the last batch's pixels are
                             not all exact in bf16 (f32x: the layer-0 GEMMs then run all 6
                             plane pairs instead of 3; bf16/f32x: the BCE target is read in
-                            fp32 instead of bf16); absent in f32 mode                      */
+                            fp32 instead of bf16); absent in f32 mode. The flag alternates
+                            between two slots batch by batch: re-fetch the pointer after
+                            each forward                                                    */
 };
 
 int mvae_abi_version(void);

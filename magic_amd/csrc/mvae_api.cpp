@@ -103,6 +103,7 @@ struct mvae_ctx {
   std::vector<PlaneBuf> planes;
   int np = 0;            // planes per buffer: 0 (fp32 mode), 1 (bf16), 3 (f32x)
   int* dyn = nullptr;    // bf16/f32x: some de-interleaved pixel not exact in bf16?
+  int* dyn_cur = nullptr;  // ... its slot of the last de-interleave (two slots, used in turn)
   int x32mask = 7;       // fp32 row blocks of xs the step reads (bit c: 0 rot, 1 lock, 2 key)
   int x32dyn = 0;        // ... written only when *dyn != 0 (the BCE target, else read as bf16)
   // schedule (each GEMM tagged with its timing region)
@@ -898,7 +899,7 @@ int mvae_buffer(mvae_ctx* ctx, int which, float** ptr, size_t* count) {
       *ptr = ctx->eps; *count = (size_t)3 * ctx->B * ctx->L; break;
     case MVAE_BUF_DYN:
       if (!ctx->dyn) return fail(ctx, MVAE_EINVAL, "no dyn flag in this precision mode");
-      *ptr = reinterpret_cast<float*>(ctx->dyn); *count = 1; break;
+      *ptr = reinterpret_cast<float*>(ctx->dyn_cur ? ctx->dyn_cur : ctx->dyn); *count = 1; break;
     default: return fail(ctx, MVAE_EINVAL, "bad buffer id");
   }
   return MVAE_OK;
@@ -953,7 +954,16 @@ int mvae_sync_params(mvae_ctx* ctx, void* stream) {
 static int run(mvae_ctx* ctx, const GemmDesc& d, hipStream_t st, int r = -1) {
   TimeScope ts(ctx, r < 0 ? region(ctx, "other_gemm") : r, st);
   const bool sd = st == ctx->side && ctx->side;
-  MV_CHECK(gemm_run(d, sd ? ctx->ws_side : ctx->ws, ctx->ws_elems, st));
+  float* ws = sd ? ctx->ws_side : ctx->ws;
+  // descriptors name the pixel flag by its first slot; the last de-interleave raised dyn_cur
+  if (ctx->dyn_cur && ctx->dyn_cur != ctx->dyn && (d.dynA == ctx->dyn || d.epi.xdyn == ctx->dyn)) {
+    GemmDesc dd = d;
+    if (dd.dynA == ctx->dyn) dd.dynA = ctx->dyn_cur;
+    if (dd.epi.xdyn == ctx->dyn) dd.epi.xdyn = ctx->dyn_cur;
+    MV_CHECK(gemm_run(dd, ws, ctx->ws_elems, st));
+    return MVAE_OK;
+  }
+  MV_CHECK(gemm_run(d, ws, ctx->ws_elems, st));
   return MVAE_OK;
 }
 
@@ -975,9 +985,13 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
   auto c = ctx;
   {
     TIMED("deinterleave");
-    if (c->dyn) MV_CHECK(hipMemsetAsync(c->dyn, 0, sizeof(int), st));
-    MV_CHECK(launch_deinterleave(x, c->xs, planes_of(c, c->xs), c->dyn, c->B, c->D, c->ldx,
-                                 c->x32mask, c->x32dyn, st));
+    // the flag's slots alternate: this pass raises the one the previous pass zeroed and zeroes
+    // the previous one (its readers are all behind on this stream), no memset launch per step
+    int* prev = c->dyn_cur ? c->dyn_cur : c->dyn;
+    int* cur = c->dyn ? (prev == c->dyn ? c->dyn + 1 : c->dyn) : nullptr;
+    MV_CHECK(launch_deinterleave(x, c->xs, planes_of(c, c->xs), cur, c->dyn ? prev : nullptr, c->B,
+                                 c->D, c->ldx, c->x32mask, c->x32dyn, st));
+    c->dyn_cur = cur;
   }
   const size_t ne = (size_t)3 * c->B * c->L;
   if (draw != ENC_MEAN) {

@@ -118,10 +118,12 @@ struct Planes {
   int n = 0;
 };
 // f32mask: bit c -> write fp32 rows of block c (0 rot, 1 lock, 2 key). Plane 0 always (when
-// xp.p); *dyn (zeroed by the caller) is set when a pixel is not a bf16 value, and only then
-// are planes 1-2 (3-plane mode) and the fp32 rows of the blocks in f32dyn_mask written.
-hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int B, int D,
-                               int ldx, int f32mask, int f32dyn_mask, hipStream_t st);
+// xp.p); *dyn (zero on entry) is set when a pixel is not a bf16 value, and only then are
+// planes 1-2 (3-plane mode) and the fp32 rows of the blocks in f32dyn_mask written. The flag has
+// two slots used in turn: each launch zeroes the other one (dyn_next, the next launch's dyn),
+// whose last readers ran before it on the stream.
+hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int* dyn_next,
+                               int B, int D, int ldx, int f32mask, int f32dyn_mask, hipStream_t st);
 // N(0,1) into out[slots][B][L]: elements (s*Bg + off + b)*L + l of the counter's global stream
 // (Bg rows per slot over all ranks, this rank's rows starting at off)
 hipError_t launch_normal(float* out, int slots, int B, int L, int Bg, int off, uint64_t seed,

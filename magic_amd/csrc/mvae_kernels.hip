@@ -55,7 +55,9 @@ __device__ __forceinline__ uint2 pack4(unsigned short a, unsigned short b, unsig
 // never pay for them; the GEMMs read the residual planes only when *dyn != 0).
 __global__ void deinterleave_vec_kernel(const float4* __restrict__ x, float* __restrict__ xs,
                                         unsigned short* __restrict__ xp, int* __restrict__ dyn,
-                                        int B, int D, int ldx, int f32mask) {
+                                        int B, int D, int ldx, int f32mask, int* __restrict__ dyn_next) {
+  // the other slot of the flag, for the next de-interleave (no per-step memset launch)
+  if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) *dyn_next = 0;
   const int b = blockIdx.y;
   const int q = blockIdx.x * blockDim.x + threadIdx.x;  // pixel quad
   bool nz = false;
@@ -89,7 +91,9 @@ __global__ void deinterleave_vec_kernel(const float4* __restrict__ x, float* __r
 template <int NQ>
 __global__ void deinterleave_vecn_kernel(const float4* __restrict__ x, float* __restrict__ xs,
                                          unsigned short* __restrict__ xp, int* __restrict__ dyn,
-                                         int B, int D, int ldx, int f32mask) {
+                                         int B, int D, int ldx, int f32mask, int* __restrict__ dyn_next) {
+  // the other slot of the flag, for the next de-interleave (no per-step memset launch)
+  if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) *dyn_next = 0;
   static_assert(NQ % 2 == 0, "whole 16-B plane stores");
   constexpr int NP = 4 * NQ;  // pixels per thread
   const int b = blockIdx.y;
@@ -138,7 +142,9 @@ __global__ void deinterleave_vecn_kernel(const float4* __restrict__ x, float* __
 
 __global__ void deinterleave_scalar_kernel(const float* __restrict__ x, float* __restrict__ xs,
                                            unsigned short* __restrict__ xp, int* __restrict__ dyn,
-                                           int B, int D, int ldx, int f32mask) {
+                                           int B, int D, int ldx, int f32mask, int* __restrict__ dyn_next) {
+  // the other slot of the flag, for the next de-interleave (no per-step memset launch)
+  if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) *dyn_next = 0;
   const int b = blockIdx.y;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   bool nz = false;
@@ -773,27 +779,27 @@ __global__ void mvae_region_marker() {}
 
 }  // namespace
 
-hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int B, int D,
-                               int ldx, int f32mask, int f32dyn_mask, hipStream_t st) {
+hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int* dyn_next,
+                               int B, int D, int ldx, int f32mask, int f32dyn_mask, hipStream_t st) {
   // pixels per thread: 8 (default), 16 or 4 (MVAE_DEINT=16 / 4, A/B)
   static const int npt = [] { const char* v = std::getenv("MVAE_DEINT"); return v ? std::atoi(v) : 8; }();
   const bool al = (reinterpret_cast<uintptr_t>(x) % 16) == 0;
   if (npt == 16 && (D % 16) == 0 && al && (ldx % 8) == 0) {
     dim3 g(nblocks(D / 16, 256), B);
     hipLaunchKernelGGL(deinterleave_vecn_kernel<4>, g, dim3(256), 0, st,
-                       reinterpret_cast<const float4*>(x), xs, xp.p, dyn, B, D, ldx, f32mask);
+                       reinterpret_cast<const float4*>(x), xs, xp.p, dyn, B, D, ldx, f32mask, dyn_next);
   } else if (npt != 4 && (D % 8) == 0 && al && (ldx % 8) == 0) {
     dim3 g(nblocks(D / 8, 256), B);
     hipLaunchKernelGGL(deinterleave_vecn_kernel<2>, g, dim3(256), 0, st,
-                       reinterpret_cast<const float4*>(x), xs, xp.p, dyn, B, D, ldx, f32mask);
+                       reinterpret_cast<const float4*>(x), xs, xp.p, dyn, B, D, ldx, f32mask, dyn_next);
   } else if ((D % 4) == 0 && (reinterpret_cast<uintptr_t>(x) % 16) == 0 && (ldx % 4) == 0) {
     dim3 g(nblocks(D / 4, 256), B);
     hipLaunchKernelGGL(deinterleave_vec_kernel, g, dim3(256), 0, st,
-                       reinterpret_cast<const float4*>(x), xs, xp.p, dyn, B, D, ldx, f32mask);
+                       reinterpret_cast<const float4*>(x), xs, xp.p, dyn, B, D, ldx, f32mask, dyn_next);
   } else {
     dim3 g(nblocks(D, 256), B);
     hipLaunchKernelGGL(deinterleave_scalar_kernel, g, dim3(256), 0, st, x, xs, xp.p, dyn, B, D, ldx,
-                       f32mask);
+                       f32mask, dyn_next);
   }
   f32dyn_mask &= ~f32mask;
   if (dyn && xp.p && (xp.n == 3 || f32dyn_mask))

@@ -296,6 +296,38 @@ def test_determinism_bitwise_f32x_splitk():
         eng.close()
 
 
+@pytest.mark.parametrize("prec", ["bf16", "f32x"])
+def test_dyn_flag_alternating_batches(prec):
+    """The inexact-pixel flag alternates between two slots batch by batch (each de-interleave
+    zeroes the other): exact and grey batches in any order give the flag and the bitwise
+    results of a fresh engine on that batch."""
+    cfg = preset("8c", image_size=30, batch=200, precision=prec)
+    P = make_params(cfg)
+    order = [True, False, False, True, True, False, True]
+    batches = {g: make_inputs(cfg, cfg.batch, seed=7, grey=g) for g in (False, True)}
+    ref = {}
+    for g in (False, True):
+        fresh = _engine(cfg)
+        try:
+            fresh.load_params(P)
+            ref[g] = gpu_phases(fresh, *batches[g])
+        finally:
+            fresh.close()
+    eng = _engine(cfg)
+    try:
+        for g in order:
+            eng.load_params(P)
+            out = gpu_phases(eng, *batches[g])
+            assert int(eng.buffer(_lib.BUF_DYN).view(torch.int32).item()) == int(g)
+            for a, b in zip(out[:2], ref[g][:2]):
+                np.testing.assert_array_equal(a, b)
+            for i in (2, 3):
+                for k in ref[g][i]:
+                    np.testing.assert_array_equal(out[i][k], ref[g][i][k])
+    finally:
+        eng.close()
+
+
 @pytest.mark.parametrize("n_enc", [1, 3])
 def test_backward_parts_match_backward(n_enc):
     """backward_part(0..2) == backward bitwise; the released ranges tile g1 and the encoder
