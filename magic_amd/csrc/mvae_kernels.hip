@@ -85,6 +85,49 @@ __global__ void deinterleave_vec_kernel(const float4* __restrict__ x, float* __r
   if (dyn && __ballot(nz) != 0 && (threadIdx.x & 63) == 0) atomicOr(dyn, 1);
 }
 
+// 4 NQ pixels (3 NQ float4 of x in v, pixel order) of row b from column col -> the fp32 rows
+// of the blocks in f32mask and bf16 plane 0 (16-B stores); returns whether a pixel is inexact
+template <int NQ>
+__device__ __forceinline__ bool deint_put(const float4* v, float* __restrict__ xs,
+                                          unsigned short* __restrict__ xp, int B, int b,
+                                          size_t col, int ldx, int f32mask) {
+  static_assert(NQ % 2 == 0, "whole 16-B plane stores");
+  constexpr int NP = 4 * NQ;
+  bool nz = false;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int ch = c == 0 ? 1 : (c == 1 ? 0 : 2);  // block c (rot, lock, key) <- channel ch
+    float f[NP];
+#pragma unroll
+    for (int h = 0; h < NQ; ++h) {
+      const float4 a = v[3 * h], bb = v[3 * h + 1], cc = v[3 * h + 2];
+      const float e[12] = {a.x, a.y, a.z, a.w, bb.x, bb.y, bb.z, bb.w, cc.x, cc.y, cc.z, cc.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) f[4 * h + j] = e[3 * j + ch];
+    }
+    const size_t o = (size_t)(c * B + b) * ldx + col;
+    if (f32mask >> c & 1) {
+#pragma unroll
+      for (int h = 0; h < NQ; ++h)
+        *reinterpret_cast<float4*>(xs + o + 4 * h) = make_float4(f[4 * h], f[4 * h + 1], f[4 * h + 2], f[4 * h + 3]);
+    }
+    if (xp) {
+#pragma unroll
+      for (int h = 0; h < NQ; h += 2) {
+        float r[8];
+        unsigned short h16[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h16[j] = bf16_rn(f[4 * h + j], r[j]);
+        const uint2 lo = pack4(h16[0], h16[1], h16[2], h16[3]), hi = pack4(h16[4], h16[5], h16[6], h16[7]);
+        *reinterpret_cast<uint4*>(xp + o + 4 * h) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) nz |= r[j] != 0.f;
+      }
+    }
+  }
+  return nz;
+}
+
 // The same for 4 NQ pixels per thread (D % (4 NQ) == 0): 3 NQ 16-B loads (48 NQ contiguous
 // bytes) issued together, then per block NQ / 2 16-B plane stores. 8 pixels per thread measured
 // 0.305 -> 0.287 ms at C3 (profiles/r4/r4y_deinterleave.txt)
@@ -94,7 +137,6 @@ __global__ void deinterleave_vecn_kernel(const float4* __restrict__ x, float* __
                                          int B, int D, int ldx, int f32mask, int* __restrict__ dyn_next) {
   // the other slot of the flag, for the next de-interleave (no per-step memset launch)
   if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) *dyn_next = 0;
-  static_assert(NQ % 2 == 0, "whole 16-B plane stores");
   constexpr int NP = 4 * NQ;  // pixels per thread
   const int b = blockIdx.y;
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -104,38 +146,7 @@ __global__ void deinterleave_vecn_kernel(const float4* __restrict__ x, float* __
     float4 v[3 * NQ];
 #pragma unroll
     for (int i = 0; i < 3 * NQ; ++i) v[i] = src[i];
-    const size_t col = (size_t)NP * q;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-      const int ch = c == 0 ? 1 : (c == 1 ? 0 : 2);  // block c (rot, lock, key) <- channel ch
-      float f[NP];
-#pragma unroll
-      for (int h = 0; h < NQ; ++h) {
-        const float4 a = v[3 * h], bb = v[3 * h + 1], cc = v[3 * h + 2];
-        const float e[12] = {a.x, a.y, a.z, a.w, bb.x, bb.y, bb.z, bb.w, cc.x, cc.y, cc.z, cc.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) f[4 * h + j] = e[3 * j + ch];
-      }
-      const size_t o = (size_t)(c * B + b) * ldx + col;
-      if (f32mask >> c & 1) {
-#pragma unroll
-        for (int h = 0; h < NQ; ++h)
-          *reinterpret_cast<float4*>(xs + o + 4 * h) = make_float4(f[4 * h], f[4 * h + 1], f[4 * h + 2], f[4 * h + 3]);
-      }
-      if (xp) {
-#pragma unroll
-        for (int h = 0; h < NQ; h += 2) {
-          float r[8];
-          unsigned short h16[8];
-#pragma unroll
-          for (int j = 0; j < 8; ++j) h16[j] = bf16_rn(f[4 * h + j], r[j]);
-          const uint2 lo = pack4(h16[0], h16[1], h16[2], h16[3]), hi = pack4(h16[4], h16[5], h16[6], h16[7]);
-          *reinterpret_cast<uint4*>(xp + o + 4 * h) = make_uint4(lo.x, lo.y, hi.x, hi.y);
-#pragma unroll
-          for (int j = 0; j < 8; ++j) nz |= r[j] != 0.f;
-        }
-      }
-    }
+    nz = deint_put<NQ>(v, xs, xp, B, b, (size_t)NP * q, ldx, f32mask);
   }
   if (dyn && __ballot(nz) != 0 && (threadIdx.x & 63) == 0) atomicOr(dyn, 1);
 }
@@ -781,7 +792,8 @@ __global__ void mvae_region_marker() {}
 
 hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int* dyn_next,
                                int B, int D, int ldx, int f32mask, int f32dyn_mask, hipStream_t st) {
-  // pixels per thread: 8 (default), 16 or 4 (MVAE_DEINT=16 / 4, A/B)
+  // pixels per thread: 8 (default), 16 or 4 (MVAE_DEINT=16 / 4, A/B); an LDS-staged form with
+  // lane-contiguous loads measured slower (profiles/r4/r4an_deinterleave_lds_rejected.txt)
   static const int npt = [] { const char* v = std::getenv("MVAE_DEINT"); return v ? std::atoi(v) : 8; }();
   const bool al = (reinterpret_cast<uintptr_t>(x) % 16) == 0;
   if (npt == 16 && (D % 16) == 0 && al && (ldx % 8) == 0) {
