@@ -571,6 +571,8 @@ def measure(args, cfg, world, rank, local, dev, *, timing, steps, warmup, keep=F
         eng.timing_select(dom)
         eng.timing_enable(True)
 
+    host_t = []
+
     def timed(n, batch_of):
         if world > 1:
             dist.barrier()
@@ -578,6 +580,8 @@ def measure(args, cfg, world, rank, local, dev, *, timing, steps, warmup, keep=F
         t0 = time.perf_counter()
         for i in range(n):
             stepper.step(*batch_of(i))
+        # host time to enqueue the steps: close to the elapsed time = launch-bound
+        host_t.append(time.perf_counter() - t0)
         if world > 1:
             dist.barrier()
         sync()
@@ -597,7 +601,8 @@ def measure(args, cfg, world, rank, local, dev, *, timing, steps, warmup, keep=F
     losses = eng.losses.cpu().numpy().tolist()
     if not np.all(np.isfinite(losses)):
         raise RuntimeError(f"non-finite losses after the timed steps: {losses}")
-    out = {"cfg": cfg, "elapsed": elapsed, "steps": steps, "regions": regions, "dom": dom,
+    out = {"cfg": cfg, "elapsed": elapsed, "host_elapsed": host_t[0], "steps": steps,
+           "regions": regions, "dom": dom,
            "dom_timed": dom_timed, "losses": losses}
     if not args.dry_run:
         out["n_all"] = eng.buffer(_lib.BUF_PARAMS).numel()
@@ -896,6 +901,7 @@ def main():
                               "value": round(c.batch * world * m["steps"] / m["elapsed"], 2),
                               "unit": "shape-pairs/s", "per_gpu_value": round(c.batch * m["steps"] / m["elapsed"], 2),
                               "ms_per_step": round(m["elapsed"] / m["steps"] * 1e3, 4),
+                              "host_ms_per_step": round(m["host_elapsed"] / m["steps"] * 1e3, 4),
                               "global_batch": c.batch * world, "per_gpu_batch": c.batch,
                               "dtype": c.precision, "overlap_mse": round(m["mse"], 2),
                               "roofline": rf, "loss_roofline": lr, "pipeline": m.get("pipeline")}
@@ -934,6 +940,7 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(head["elapsed"] / args.steps * 1e3, 4),
+            "host_ms_per_step": round(head["host_elapsed"] / args.steps * 1e3, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
