@@ -558,8 +558,10 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   // eight-phase kernel wherever a 256-row kernel would run (2)
   int e8_mode = 1;
   if (const char* e8 = std::getenv("MVAE_E8"); e8 && (*e8 == '0' || *e8 == '2')) e8_mode = *e8 - '0';
-  bool thin_ring = true;    // MVAE_THIN_RING=0: the f32x latent head on the VALU kernel (A/B)
-  if (const char* tr = std::getenv("MVAE_THIN_RING"); tr && *tr == '0') thin_ring = false;
+  // MVAE_THIN_RING=0: the f32x latent head on the VALU kernel, 1: the head's weight gradient on
+  // the fp32 kernel (A/B); default 2
+  int thin_ring = 2;
+  if (const char* tr = std::getenv("MVAE_THIN_RING"); tr && (*tr == '0' || *tr == '1')) thin_ring = *tr - '0';
   bool dact_planes = true;  // MVAE_DACT_F32AUX=1: bf16-mode DACT reads the fp32 activations (A/B)
   if (const char* fa = std::getenv("MVAE_DACT_F32AUX"); fa && *fa == '1') dact_planes = false;
   const int gp = cfg->precision == MVAE_PREC_BF16 ? GEMM_BF16
@@ -607,9 +609,11 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     // ... except the f32x latent head at small L over the tall stacked rows (C2: forward
     // 12288 x 40 x 501, dgrad 16384 x 500 x 40): the ring kernel's plane products (variant 3, any
     // shape) beat the VALU kernel there (24.3 / 23.9 us vs 30.8 / 38.0 us in the step,
-    // profiles/r4/r4g_plan_c2.txt and bench_default_r4p_regions.txt)
+    // profiles/r4/r4g_plan_c2.txt and bench_default_r4p_regions.txt), and its weight gradient
+    // (501 x 40 x 8192, two products: 35.6 vs 40.7 us on the fp32 kernel, r4ar_thin_gemms.txt)
     const int lo = d.M < d.N ? d.M : d.N;
-    if (gp == GEMM_F32X && e8_mode == 1 && !wide_shape && d.M >= 4096 && lo >= 32 && d.K >= 32 &&
+    const bool tall = d.M >= 4096 || (thin_ring == 2 && d.K >= 4096);
+    if (gp == GEMM_F32X && e8_mode == 1 && !wide_shape && tall && lo >= 32 && d.K >= 32 &&
         d.variant == 0 && thin_ring)
       d.variant = 3;
     if (c->valu && gemm_valu_fits(d) && !(gp != GEMM_F32 && wide_shape)) {
