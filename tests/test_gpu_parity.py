@@ -70,7 +70,7 @@ def _padded(rows, cols, g):
                                            (300, 517, 1001, 7), (513, 260, 130, 7), (40, 70, 200, 7),
                                            (256, 256, 64, 7), (300, 517, 1001, 6), (1000, 600, 4099, 11),
                                            (513, 260, 130, 11), (300, 517, 1001, 11), (1000, 600, 4099, 12),
-                                           (2100, 500, 700, 11)])
+                                           (2100, 500, 700, 11), (501, 40, 8193, 3)])
 def test_gemm_wide_kernel(at, bt, M, N, K, variant, prec):
     """The 256-row LDS-DMA bf16 kernels (variant 3 forces the interleaved ring kernel; 0 lets the
     planner pick it and its tile N for M, N >= 256; 11 / 12 force tile N 128 / 256; 6 is the round-1
@@ -297,11 +297,12 @@ def test_determinism_bitwise_f32x_splitk():
 
 
 @pytest.mark.parametrize("prec", ["bf16", "f32x"])
-def test_dyn_flag_alternating_batches(prec):
+@pytest.mark.parametrize("image", [30, 40])  # 900 pixels: 4-pixel kernel; 1600: 8-pixel kernel
+def test_dyn_flag_alternating_batches(prec, image):
     """The inexact-pixel flag alternates between two slots batch by batch (each de-interleave
     zeroes the other): exact and grey batches in any order give the flag and the bitwise
     results of a fresh engine on that batch."""
-    cfg = preset("8c", image_size=30, batch=200, precision=prec)
+    cfg = preset("8c", image_size=image, batch=200, precision=prec)
     P = make_params(cfg)
     order = [True, False, False, True, True, False, True]
     batches = {g: make_inputs(cfg, cfg.batch, seed=7, grey=g) for g in (False, True)}
