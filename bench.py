@@ -76,6 +76,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive h2d leg")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="skip the input-pipeline leg (inputs() -> HIP batch producer -> step)")
+    ap.add_argument("--plan", action="store_true",
+                    help="print the per-rank plan of a --gpus N run (configs, batches, collectives) "
+                         "as one JSON line and exit: no ranks, no GPU")
     ap.add_argument("--dry-run", action="store_true",
                     help="CPU rehearsal of the launcher / data-parallel / timing / JSON path "
                          "(gloo, a stand-in engine; no GPU, no kernels, not a measurement)")
@@ -792,10 +795,57 @@ def workload(args_config, cfg):
             f"{'reciprocal ' if cfg.reciprocal else ''}{cfg.metric}")
 
 
+# ------------------------------------------------------------------------ plan
+def run_plan(args) -> dict:
+    """What ``bench.py --gpus N`` runs on each rank (``--plan``): the headline and configs-block
+    workloads with their per-rank and global batches, and the data-parallel exchange per step
+    (DataParallelStep: cosine colsq / coldot, the async loss reduce, the gradient bucket in
+    backward parts with the layer-0 rows in ``wgrad0_chunks`` chunks). No GPU is touched."""
+    from magic_amd.config import baseline_config
+
+    N = args.gpus
+    ids = [args.config] + ([] if args.no_configs else
+                           [c for c in (["C3", "C5"] if N == 1 else ["C4", "C5"])
+                            if c != args.config and not (c == "C4" and args.config == "C3")])
+    out = {"n_gpus": N, "launcher": "torch.distributed.run, one process per GPU" if N > 1 else "one process",
+           "backend": "nccl (RCCL over xGMI)" if N > 1 else None, "configs": {}}
+    for cid in ids:
+        cfg = baseline_config("C3" if cid == "C4" else cid)
+        if cid == args.config and args.batch:
+            cfg = cfg.replace(batch=args.batch)
+        if cid == args.config and args.precision:
+            cfg = cfg.replace(precision=args.precision)
+        e, L = list(cfg.enc), cfg.latent
+        widths = [cfg.D] + e
+        enc = sum((widths[i] + 1) * widths[i + 1] for i in range(len(e))) + (e[-1] + 1) * 2 * L
+        dec = (L + 1) * cfg.dec[0] + (cfg.dec[0] + 1) * cfg.dec[1] + (cfg.dec[1] + 1) * cfg.D
+        g1, g2 = enc + dec, enc
+        chunks = 4 if N > 1 else 1
+        out["configs"][cid] = {
+            "workload": workload("C3" if cid == "C4" else cid, cfg),
+            "per_rank_batch": cfg.batch, "global_batch": cfg.batch * N, "precision": cfg.precision,
+            "metric": ("reciprocal " if cfg.reciprocal else "") + cfg.metric,
+            "wgrad0_chunks": chunks,
+            "per_step_collectives": ([] if N == 1 else
+                                     (["all_reduce colsq (%d floats, blocking)" % (2 * L),
+                                       "all_reduce coldot (%d floats, blocking)" % L]
+                                      if cfg.metric == "cosine" else []) +
+                                     ["all_reduce losses (5 floats, async)",
+                                      "all_reduce gradient bucket [g1|g2] %.1f MB fp32 in %d async parts "
+                                      "(decoder; layer-0 rows x %d chunks; rest of the encoder)"
+                                      % ((g1 + g2) * 4e-6, chunks + 2, chunks)]),
+            "params_approx": g1,
+        }
+    return out
+
+
 # ------------------------------------------------------------------------ main
 def main():
     argv = sys.argv[1:]
     args = parse_args(argv)
+    if args.plan:
+        print(json.dumps(run_plan(args)), flush=True)
+        return
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args, argv))

@@ -716,7 +716,10 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
   // dgrad, 86 vs 64 tiles, stays on the eight-phase kernel: 0.107 vs 0.115 ms in r4n)
   const bool ring_fills = t192 && np == 1 && tl192 > 128 && tl192 <= 256 && 3 * tl192 >= 4 * t256;
   const bool e8_rule = big && t256 >= 32 && (t256 >= 256 || (long long)np * kt >= 64) && !ring_fills;
-  const bool allow_e8 = force_e8 || (d.variant == 0 && e8_rule);
+  // the eight-phase kernel addresses an operand plane by 32-bit per-lane element offsets
+  const long long ea = (long long)(d.at ? d.K : d.M) * d.lda, eb = (long long)(d.bt ? d.N : d.K) * d.ldb;
+  const bool e8_fits = ea < (1LL << 32) && eb < (1LL << 32);
+  const bool allow_e8 = e8_fits && (force_e8 || (d.variant == 0 && e8_rule));
   double best = 1e30;
   WidePlan pl;
   for (int cand = 0; cand < 5; ++cand) {
@@ -724,7 +727,7 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
     const bool e8 = cand == 2;
     const int w = cand == 0 || cand == 3 ? 256 : cand == 1 || cand == 4 ? 128 : TN_E8;
     const int tmr = cand >= 3 ? 192 : 256;
-    if (e8 ? !allow_e8 : (force_e8 || allow_e8)) continue;
+    if (e8 ? !allow_e8 : allow_e8 || (force_e8 && e8_fits)) continue;
     if (cand >= 3 && !t192) continue;
     if ((d.tm == 192 && t192 && cand != 3 && cand != 4) || (d.tm == 256 && cand >= 3)) continue;
     if (d.variant == 11 && w != 128) continue;

@@ -1188,9 +1188,11 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
     }
     // early Adam: the side stream's Adam of the blocks after layer 0 (mvae_adam) may start once
     // the dgrad chain -- the last reader of their weights -- is done, beside the layer-0
-    // weight gradient
+    // weight gradient. Only in the single-call mvae_backward (join_dec false): a caller of
+    // mvae_backward_part all-reduces the gradients between the parts and mvae_adam, and the side
+    // stream is not ordered after those collectives
     c->early_fork = false;
-    if (c->early_adam && two) {
+    if (c->early_adam && two && !join_dec) {
       if ((rc = fork())) return rc;
       c->early_fork = true;
     }
@@ -1243,7 +1245,8 @@ extern "C" int mvae_set_option(mvae_ctx* ctx, const char* name, int value) {
   }
   if (k == "early_adam") {
     // only for callers that do not touch the gradients between mvae_backward and mvae_adam (no
-    // all-reduce): the side stream reads them as soon as the backward has written them
+    // all-reduce): the side stream reads them as soon as the backward has written them. Taken by
+    // mvae_backward only; the per-part API (mvae_backward_part, the all-reduce path) ignores it
     if (ctx->phase == 4) return fail(ctx, MVAE_ESTATE, "early_adam cannot change mid-backward");
     ctx->early_adam = value != 0;
     return MVAE_OK;

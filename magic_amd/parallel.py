@@ -71,6 +71,10 @@ class DataParallelStep:
             # 2.005 ms, so f32x only; MVAE_NO_EARLY_ADAM=1: one Adam launch after the backward
             engine.set_option("early_adam", 1)
             self._early_set = True
+        elif self.coll and hasattr(engine, "set_option"):
+            # collectives between backward and adam: never Adam on the side stream (an engine an
+            # earlier collective-free DataParallelStep left with the option on)
+            engine.set_option("early_adam", 0)
         if hasattr(engine, "set_shard"):
             # the internal eps sampler draws this rank's rows of the global batch's stream,
             # so a sharded step without explicit eps equals the single-process step too

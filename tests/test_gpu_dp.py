@@ -16,28 +16,103 @@ from tests.gpu_helpers import make_inputs, make_params, max_rel
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, metric, q, conv=False, size=24, chunks=4):
+def _worker(rank, world, port, metric, q, conv=False, size=24, chunks=4, cfg=None, early=False):
     import torch.distributed as dist
     from magic_amd.engine import Engine
     from magic_amd.parallel import DataParallelStep
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    cfg = preset("8c", image_size=size, batch=32, metric=metric, conv=conv)
+    cfg = cfg or preset("8c", image_size=size, batch=32, metric=metric, conv=conv)
     B = cfg.batch
     half = B // world
     eng = Engine(cfg.replace(batch=half, global_batch=B), 0)
     eng.load_params(make_params(cfg))
     X, areas, eps = make_inputs(cfg, B)
     sl = slice(rank * half, (rank + 1) * half)
+    if early:  # an engine left with Adam-on-the-side-stream on (e.g. by a collective-free step)
+        eng.set_option("early_adam", 1)
     st = DataParallelStep(eng, wgrad0_chunks=chunks)
     if chunks > 1:
         assert eng.N_BACKWARD_PARTS > 3  # the layer-0 weight gradient really runs in row chunks
     st.step(torch.from_numpy(X[sl]).cuda(), torch.from_numpy(areas[sl]).cuda(),
             torch.from_numpy(np.ascontiguousarray(eps[:, sl])).cuda())
     torch.cuda.synchronize()
-    q.put((rank, eng.grads.cpu().numpy(), eng.losses.cpu().numpy()))
+    q.put((rank, eng.grads.cpu().numpy(), eng.losses.cpu().numpy(),
+           {k: v.cpu().numpy() for k, v in eng.params().items()}))
     eng.close()
     dist.destroy_process_group()
+
+
+def _dp2(cfg, metric="cosine", chunks=4, early=False):
+    """2 spawned gloo ranks on this GPU, each half of cfg.batch: {rank: (grads, losses, params)}"""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, metric, q),
+                         kwargs=dict(chunks=chunks, cfg=cfg, early=early)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict((r, (g, l, P)) for r, g, l, P in (q.get(timeout=600) for _ in range(2)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    return res
+
+
+def _single(cfg):
+    """one process on the whole batch: grads, losses, and the parameters after Adam"""
+    from magic_amd.engine import Engine
+    eng = Engine(cfg, 0)
+    eng.load_params(make_params(cfg))
+    X, areas, eps = make_inputs(cfg, cfg.batch)
+    eng.forward(torch.from_numpy(X).cuda(), torch.from_numpy(eps).cuda())
+    eng.metric(torch.from_numpy(areas).cuda())
+    eng.backward()
+    torch.cuda.synchronize()
+    g, l = eng.grads.cpu().numpy(), eng.losses.cpu().numpy()
+    eng.adam()
+    P = {k: v.cpu().numpy() for k, v in eng.params().items()}
+    eng.close()
+    return g, l, P
+
+
+@pytest.mark.parametrize("prec", ["f32x", "f32"])
+def test_dp2_early_adam_left_on_waits_for_the_all_reduce(prec):
+    """An engine whose early_adam option was left on: a collective step must not run
+    Adam on the side stream before the gradient all-reduce -- both replicas end bitwise equal,
+    and equal to the single-process step on the whole batch (1e-4)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    cfg = preset("8c", image_size=24, batch=32, precision=prec)
+    g_ref, l_ref, P_ref = _single(cfg)
+    res = _dp2(cfg, early=True)
+    for k in P_ref:
+        np.testing.assert_array_equal(res[0][2][k], res[1][2][k])
+        assert max_rel(res[0][2][k], P_ref[k]) <= 1e-4, k
+    assert max_rel(res[0][0], g_ref) <= 1e-4
+
+
+def test_dp2_c4_per_rank_shape_matches_full_batch():
+    """BASELINE C4's per-rank workload through DataParallelStep on this GPU: 2 gloo ranks at C3's
+    shape each (8d, L = 200, bf16, B = 8192 per rank, wgrad0_chunks = 4, cosine colsq / coldot
+    all-reduces, async loss reduce) against one process on the concatenated 16 384-pair batch:
+    losses and the whole all-reduced gradient bucket at the documented bf16 bar."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from magic_amd.config import baseline_config
+    cfg = baseline_config("C3").replace(batch=16384)
+    g_ref, l_ref, _ = _single(cfg)
+    res = _dp2(cfg, chunks=4)
+    for r in range(2):
+        g, l, _ = res[r]
+        np.testing.assert_allclose(l, l_ref, rtol=2e-3)
+        err = max_rel(g, g_ref)
+        print(f"C4 per-rank shape, rank {r}: losses {l.tolist()} vs {l_ref.tolist()}; bucket max-rel {err:.3e}")
+        assert err <= 5e-2, err
+    np.testing.assert_array_equal(res[0][0], res[1][0])
 
 
 @pytest.mark.parametrize("metric,conv,size,chunks", [("cosine", False, 24, 4), ("sqdiff", False, 24, 4),
@@ -69,7 +144,7 @@ def test_dp2_on_gpu_matches_full_batch(metric, conv, size, chunks):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, metric, q, conv, size, chunks)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r, (g, l)) for r, g, l in (q.get(timeout=300) for _ in range(2)))
+    res = dict((r, (g, l)) for r, g, l, _ in (q.get(timeout=300) for _ in range(2)))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -75,6 +75,7 @@ struct Args {
   unsigned short* C;
   int M, N, K;
   unsigned long long* stamps;
+  int gm;  // m-tiles per tile group (the guide's 4; the library's 8)
 };
 
 template <bool ST>
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(NT, 1) void gemm8p_kernel(Args a) {
   // bijective XCD remap (blocks b and b + 8 share an XCD), then groups of 4 m-tiles
   const int orig = blockIdx.x, xcd = orig % 8, q = nwg / 8, r = nwg % 8;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-  constexpr int GM = 4;
+  const int GM = a.gm;
   const int grp = wg / (GM * ntn), first = grp * GM, gsz = min(ntm - first, GM);
   const int tm = first + (wg % (GM * ntn)) % gsz, tn = (wg % (GM * ntn)) / gsz;
   const int m0 = tm * 256, n0 = tn * 256;
@@ -300,13 +301,14 @@ static float from_bf16(unsigned short h) {
 typedef int (*bench_fn)(int, int, int, int, int, int, int, int, void*, float*);
 
 int main(int argc, char** argv) {
-  int M = 4096, N = 4096, K = 4096, rounds = 5, iters = 50;
+  int M = 4096, N = 4096, K = 4096, rounds = 5, iters = 50, gm = 4;
   const char* libpath = nullptr;
   int pos = 0;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--rounds")) rounds = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--iters")) iters = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--lib")) libpath = argv[++i];
+    else if (!strcmp(argv[i], "--gm")) gm = atoi(argv[++i]);
     else if (pos == 0) { M = atoi(argv[i]); ++pos; }
     else if (pos == 1) { N = atoi(argv[i]); ++pos; }
     else if (pos == 2) { K = atoi(argv[i]); ++pos; }
@@ -337,7 +339,7 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(dB, hB.data(), nb * 2, hipMemcpyHostToDevice));
   hipStream_t st;
   CK(hipStreamCreate(&st));
-  Args a{dA, dB, dC, M, N, K, dS};
+  Args a{dA, dB, dC, M, N, K, dS, gm};
 
   // correctness: every output against the naive kernel
   hipLaunchKernelGGL(ref_kernel, dim3((N + 63) / 64, (M + 3) / 4), dim3(256), 0, st, dA, dB, dR, M, N, K);
