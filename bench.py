@@ -71,6 +71,8 @@ def parse_args(argv=None):
     ap.add_argument("--pmc-child", default="", help=argparse.SUPPRESS)
     ap.add_argument("--opt", action="append", default=[],
                     help="libmvae schedule switch NAME=VALUE (mvae_set_option), repeatable")
+    ap.add_argument("--create-opt", action="append", default=[],
+                    help="libmvae plan-time kernel switch NAME=VALUE (mvae_create_ex), repeatable")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the configs block (C3 / C5 on one GPU; C4 / C5 with N ranks)")
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive h2d leg")
@@ -882,7 +884,7 @@ def main():
             cfg = cfg.replace(batch=min(cfg.batch, 16), image_size=12, latent=min(cfg.latent, 16))
         # one seed on every rank: each rank's internal sampler draws its own rows of the global
         # batch's eps stream (Engine.set_shard via DataParallelStep)
-        return cfg.replace(global_batch=cfg.batch * world)
+        return cfg.replace(global_batch=cfg.batch * world, options=",".join(args.create_opt))
 
     cfg = config_of(args.config, args.batch, args.precision)
     timing = not (args.no_timing or args.dry_run or args.pmc_child)

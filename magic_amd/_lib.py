@@ -55,6 +55,7 @@ _SIGS = {
     "mvae_abi_version": ([], C.c_int),
     "mvae_build_id": ([], C.c_char_p),
     "mvae_create": ([C.POINTER(mvae_cfg), C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "mvae_create_ex": ([C.POINTER(mvae_cfg), C.c_int, C.c_char_p, C.POINTER(C.c_void_p)], C.c_int),
     "mvae_destroy": ([C.c_void_p], C.c_int),
     "mvae_last_error": ([C.c_void_p], C.c_char_p),
     "mvae_param_count": ([C.c_void_p], C.c_int),

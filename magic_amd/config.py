@@ -30,6 +30,9 @@ class MVAEConfig:
     precision: str = "f32"
     seed: int = 2
     conv: bool = False   # conv-encoder variant: CifarNet tower (6b/net.py:50-60) before the FC encoder
+    # plan-time kernel switches of libmvae (mvae_create_ex options, "name=value,..."; A/B and
+    # tests: e8, thin_ring, valu, dact_planes, bce_split, plan_log, conv2_*); "" = measured defaults
+    options: str = ""
 
     @property
     def D(self) -> int:

@@ -683,14 +683,6 @@ bool gemm_bf16_wide(const GemmDesc& d) {
 // fp32 slab round trip and the reduction launch. Variants 11 / 12 force the ring kernel at tile
 // N 128 / 256, 13 / 14 the eight-phase kernel, 15 the ring kernels only.
 struct WidePlan { int split = 1; int tn = 256; int tm = 256; };
-// MVAE_TM192=0 (A/B): plan the ring kernels at 256-row tiles only
-static bool tm192_enabled() {
-  static const bool on = [] {
-    const char* v = std::getenv("MVAE_TM192");
-    return !(v && *v == '0');
-  }();
-  return on;
-}
 static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
   const bool fixed = d.epi.mode == EPI_BCE || d.epi.mode == EPI_BCEB || d.epi.mode == EPI_SIGMOID;
   const int kt = (d.K + 63) / 64;
@@ -706,7 +698,7 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
   // iterations copy both operand images (the ring kernel reuses an unchanged image)
   const long long t256 = (long long)((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
   // 192-row ring tiles: k-contiguous A, epilogues other than the BCE head / sigmoid
-  const bool t192 = tm192_enabled() && !d.at && d.epi.mode != EPI_BCE && d.epi.mode != EPI_BCEB &&
+  const bool t192 = !d.at && d.epi.mode != EPI_BCE && d.epi.mode != EPI_BCEB &&
                     d.epi.mode != EPI_SIGMOID;
   const long long tl192 = (long long)((d.M + 191) / 192) * ((d.N + 255) / 256) * d.batch;
   // ... except (in-step A/B, profiles/r4/README.md) single-product GEMMs where one round of
@@ -775,8 +767,8 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   // tile order: bands of 8 m-tiles walked n by n when a row has >= 8 n-tiles, so the 32 tiles
   // an XCD holds at once share 8 A and 4 B tiles in its L2 (C5 latent-head forward
   // 24576 x 4000 x 501: 0.177 -> 0.161 ms; neutral on the BCE head and the other shapes,
-  // profiles/r4/r4u_tile_group.txt); MVAE_TILE_GROUP=G overrides (A/B)
-  static const int tile_group = [] { const char* v = std::getenv("MVAE_TILE_GROUP"); return v ? std::atoi(v) : -1; }();
+  // profiles/r4/r4u_tile_group.txt); GemmDesc::group >= 0 overrides (A/B: mvae_bench_gemm)
+  const int tile_group = d.group;
   // plane pairs (i, j), i + j < max(nA, nB); the pairs with i = 0 first, j snaking (ascending for
   // even i, descending for odd i): (0,0) (0,1) (0,2) (1,1) (1,0) (2,0), so consecutive pairs share
   // the B plane at both A-plane changes and the ring kernel copies 3 A + 5 B images per k-tile

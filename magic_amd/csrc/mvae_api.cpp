@@ -394,11 +394,65 @@ int mvae_destroy(mvae_ctx* ctx) {
   return MVAE_OK;
 }
 
+// Plan-time kernel switches of one context (mvae_create_ex options; the library reads no
+// environment outside its diagnostics entry points). Defaults are the measured best plans.
+struct CreateOpts {
+  int e8 = 1;           // 256-row bf16 GEMMs: 1 planner (eight-phase + ring kernels), 0 ring only,
+                        // 2 the eight-phase kernel wherever a 256-row kernel runs
+  int thin_ring = 2;    // f32x latent head: 2 ring kernel incl. its weight gradient, 1 weight
+                        // gradient on the fp32 kernel, 0 the VALU kernel
+  int valu = 1;         // skinny products on the fp32 VALU kernel
+  int dact_planes = 1;  // bf16 mode: DACT epilogues read the activation's bf16 plane
+  int bce_split = 1;    // the BCE head in whole rounds + 256x128 ring tiles
+  int plan_log = 0;     // print the GEMM plans on stderr
+  int conv2_nw = 8, conv2_tpb = 1, conv2_fpw = 2, conv2_wg = 8, conv2_half = 1, conv2_nchunk = 0;
+};
+
+static int parse_opts(const char* s, CreateOpts* o) {
+  if (!s) return MVAE_OK;
+  std::string all(s);
+  size_t i = 0;
+  while (i < all.size()) {
+    size_t j = all.find(',', i);
+    if (j == std::string::npos) j = all.size();
+    const std::string kv = all.substr(i, j - i);
+    i = j + 1;
+    if (kv.empty()) continue;
+    const size_t eq = kv.find('=');
+    if (eq == std::string::npos) return fail(nullptr, MVAE_EINVAL, "option without '=': " + kv);
+    const std::string k = kv.substr(0, eq);
+    char* end = nullptr;
+    const long v = std::strtol(kv.c_str() + eq + 1, &end, 10);
+    if (end == kv.c_str() + eq + 1 || *end) return fail(nullptr, MVAE_EINVAL, "option value not an integer: " + kv);
+    auto in = [&](long lo, long hi) { return v >= lo && v <= hi; };
+    if (k == "e8" && in(0, 2)) o->e8 = (int)v;
+    else if (k == "thin_ring" && in(0, 2)) o->thin_ring = (int)v;
+    else if (k == "valu" && in(0, 1)) o->valu = (int)v;
+    else if (k == "dact_planes" && in(0, 1)) o->dact_planes = (int)v;
+    else if (k == "bce_split" && in(0, 1)) o->bce_split = (int)v;
+    else if (k == "plan_log" && in(0, 1)) o->plan_log = (int)v;
+    else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
+    else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
+    else if (k == "conv2_fpw" && (v == 2 || v == 4)) o->conv2_fpw = (int)v;
+    else if (k == "conv2_wg" && (v == 4 || v == 8)) o->conv2_wg = (int)v;
+    else if (k == "conv2_half" && in(0, 1)) o->conv2_half = (int)v;
+    else if (k == "conv2_nchunk" && in(0, 1 << 20)) o->conv2_nchunk = (int)v;
+    else return fail(nullptr, MVAE_EINVAL, "unknown option or value out of range: " + kv);
+  }
+  return MVAE_OK;
+}
+
 int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
+  return mvae_create_ex(cfg, device, nullptr, out);
+}
+
+int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ctx** out) {
   if (!out) return fail(nullptr, MVAE_EINVAL, "out is NULL");
   *out = nullptr;
   int rc = validate(cfg);
   if (rc) return rc;
+  CreateOpts opt;
+  if ((rc = parse_opts(options, &opt))) return rc;
   mvae_ctx* ctx = new (std::nothrow) mvae_ctx();
   if (!ctx) return fail(nullptr, MVAE_EINVAL, "out of host memory");
   ctx->cfg = *cfg;
@@ -504,13 +558,13 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     ConvTower& T = c->tower;
     const size_t a1 = (size_t)T.S1 * T.S1 * 64, a2n = (size_t)T.S2 * T.S2 * 64;
     T.mfma = cfg->precision == MVAE_PREC_BF16;
-    // kernel-shape A/B switches (diagnostics): MVAE_CONV2_HALF=0 (full-channel forward / data
-    // gradient kernel, shaped by MVAE_CONV2_NW=4|16, MVAE_CONV2_TPB=2, MVAE_CONV2_FPW=4), MVAE_CONV2_WG=4
-    if (const char* nw = std::getenv("MVAE_CONV2_NW"); nw && (*nw == '4' || nw[0] == '1')) T.conv2_nw = *nw == '4' ? 4 : 16;
-    if (const char* tp = std::getenv("MVAE_CONV2_TPB"); tp && *tp == '2') T.conv2_tpb = 2;
-    if (const char* fp = std::getenv("MVAE_CONV2_FPW"); fp && *fp == '4') T.conv2_fpw = 4;
-    if (const char* wg = std::getenv("MVAE_CONV2_WG"); wg && *wg == '4') T.conv2_wg8 = false;
-    if (const char* hf = std::getenv("MVAE_CONV2_HALF"); hf && *hf == '0') T.conv2_half = false;
+    // kernel-shape options (A/B): conv2_half=0 (full-channel forward / data gradient kernel,
+    // shaped by conv2_nw=4|16, conv2_tpb=2, conv2_fpw=4), conv2_wg=4
+    T.conv2_nw = opt.conv2_nw;
+    T.conv2_tpb = opt.conv2_tpb;
+    T.conv2_fpw = opt.conv2_fpw;
+    T.conv2_wg8 = opt.conv2_wg == 8;
+    T.conv2_half = opt.conv2_half != 0;
     ALLOC(c->xf, 3 * B * c->ldf);
     ALLOC(c->dxf, 4 * B * c->ldf);
     ALLOC(T.p1, 3 * B * a1);
@@ -533,7 +587,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     // image chunks of the MFMA weight gradient: 64 -> 256 workgroups at C5CONV, one per CU
     // (same box: 1.085 ms vs 1.11 at 128 and 1.17 at 256, profiles/r2/conv2_wgrad_ab.txt)
     T.nchunk2m = std::min(B2, 64);
-    if (const char* nc = std::getenv("MVAE_CONV2_NCHUNK"); nc && std::atoi(nc) > 0) T.nchunk2m = std::min(B2, std::atoi(nc));
+    if (opt.conv2_nchunk > 0) T.nchunk2m = std::min(B2, opt.conv2_nchunk);
     const size_t s1 = (size_t)2 * T.nchunk1 * 26 * 64;
     const size_t s2 = (size_t)2 * (T.mfma ? T.nchunk2m : T.nchunk2) * (25 * 64 + 1) * 64;
     ALLOC(T.slab, std::max(s1, s2));
@@ -552,18 +606,15 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
     return (int)e;
   }
   build_schedule(c);
-  if (const char* nv = std::getenv("MVAE_NO_VALU"); nv && *nv == '1') c->valu = false;
-  // kernel A/B switch (diagnostics), MVAE_E8: the 256-row bf16 DMA GEMMs are planned over the
-  // eight-phase and ring kernels (default, 1), on the ring kernels only (0), or on the
-  // eight-phase kernel wherever a 256-row kernel would run (2)
-  int e8_mode = 1;
-  if (const char* e8 = std::getenv("MVAE_E8"); e8 && (*e8 == '0' || *e8 == '2')) e8_mode = *e8 - '0';
-  // MVAE_THIN_RING=0: the f32x latent head on the VALU kernel, 1: the head's weight gradient on
+  if (!opt.valu) c->valu = false;
+  // option e8: the 256-row bf16 DMA GEMMs are planned over the eight-phase and ring kernels
+  // (default, 1), on the ring kernels only (0), or on the eight-phase kernel wherever a 256-row
+  // kernel would run (2)
+  const int e8_mode = opt.e8;
+  // option thin_ring: 0 the f32x latent head on the VALU kernel, 1 the head's weight gradient on
   // the fp32 kernel (A/B); default 2
-  int thin_ring = 2;
-  if (const char* tr = std::getenv("MVAE_THIN_RING"); tr && (*tr == '0' || *tr == '1')) thin_ring = *tr - '0';
-  bool dact_planes = true;  // MVAE_DACT_F32AUX=1: bf16-mode DACT reads the fp32 activations (A/B)
-  if (const char* fa = std::getenv("MVAE_DACT_F32AUX"); fa && *fa == '1') dact_planes = false;
+  const int thin_ring = opt.thin_ring;
+  const bool dact_planes = opt.dact_planes != 0;  // 0: bf16-mode DACT reads the fp32 activations (A/B)
   const int gp = cfg->precision == MVAE_PREC_BF16 ? GEMM_BF16
                  : (cfg->precision == MVAE_PREC_F32X ? GEMM_F32X : GEMM_F32);
   c->np = gp == GEMM_BF16 ? 1 : (gp == GEMM_F32X ? 3 : 0);
@@ -727,8 +778,8 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
      // 256 CUs (C2: 16 x 40 = 640 tiles = 2.5 rounds), the columns of the whole rounds run as one
      // launch and the rest as 256x128 ring tiles (half the work per tile, so the last round takes
      // about half as long); elementwise the same results and the same 128-column row partials.
-     // MVAE_BCE_SPLIT=0: never; option "bce_split" 0: one launch (A/B, tests)
-    static const bool on = [] { const char* v = std::getenv("MVAE_BCE_SPLIT"); return !(v && *v == '0'); }();
+     // create option bce_split=0: never; set_option "bce_split" 0: one launch (A/B, tests)
+    const bool on = opt.bce_split != 0;
     const GemmDesc& f = c->f_out;
     const long long tm = (f.M + 255) / 256, tn = (f.N + 255) / 256, tiles = tm * tn;
     const long long n1 = (tiles / 256) * 256 / tm;  // n-tiles of the whole rounds
@@ -766,7 +817,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out) {
   wsz(c->f_out);
   if (c->conv) wsz(c->bwd_feat);
   c->ws_elems = ws;
-  if (const char* lg = std::getenv("MVAE_PLAN_LOG"); lg && *lg == '1') {
+  if (opt.plan_log) {
     // the GEMM plans of this context (diagnostics): shape, arithmetic, kernel, split-K + combine
     auto show = [&](const GemmDesc& d, int r) {
       const int sp = gemm_plan_split(d, ws);
@@ -1584,6 +1635,8 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   d.diag = (variant >> 12) & 255; // kernel timing diagnostics (results meaningless; 32: A/B switch)
   // MVAE_BENCH_SPLIT (diagnostics): split-K forced (0 / unset: the planner's)
   if (const char* sp = std::getenv("MVAE_BENCH_SPLIT"); sp && std::atoi(sp) > 0) d.split = std::atoi(sp);
+  // MVAE_BENCH_TILE_GROUP (diagnostics): the bf16 DMA kernels' tile order (m-tiles per band)
+  if (const char* tg = std::getenv("MVAE_BENCH_TILE_GROUP"); tg && std::atoi(tg) >= 0) d.group = std::atoi(tg);
   unsigned short* planes = nullptr;
   const int np = d.prec == GEMM_F32 ? 0 : (d.prec == GEMM_BF16 ? 1 : 3);
   hipError_t e = hipMalloc(&A, na * 4);
@@ -1773,12 +1826,16 @@ extern "C" int mvae_debug_conv2(int S1, int B, int mode, int mfma, const float* 
   hipStream_t st = (hipStream_t)stream;
   ConvTower T;
   T.S1 = S1; T.S = 2 * S1; T.S2 = S1 / 2;
-  T.mfma = mfma != 0;
-  if (const char* nw = std::getenv("MVAE_CONV2_NW"); nw && (*nw == '4' || nw[0] == '1')) T.conv2_nw = *nw == '4' ? 4 : 16;
-  if (const char* tp = std::getenv("MVAE_CONV2_TPB"); tp && *tp == '2') T.conv2_tpb = 2;
-  if (const char* fp = std::getenv("MVAE_CONV2_FPW"); fp && *fp == '4') T.conv2_fpw = 4;
-  if (const char* wg = std::getenv("MVAE_CONV2_WG"); wg && *wg == '4') T.conv2_wg8 = false;
-  if (const char* hf = std::getenv("MVAE_CONV2_HALF"); hf && *hf == '0') T.conv2_half = false;
+  // mfma bit 0: the MFMA kernels; the kernel form (the create options' conv2_*): bit 1 the
+  // full-channel forward / data-gradient kernel, bits 2 / 3 its 4 / 16 waves, bit 4 two taps per
+  // slot, bit 5 four M-fragments per wave, bit 6 the 4-wave weight-gradient kernel
+  T.mfma = (mfma & 1) != 0;
+  if (mfma & 2) T.conv2_half = false;
+  if (mfma & 4) T.conv2_nw = 4;
+  if (mfma & 8) T.conv2_nw = 16;
+  if (mfma & 16) T.conv2_tpb = 2;
+  if (mfma & 32) T.conv2_fpw = 4;
+  if (mfma & 64) T.conv2_wg8 = false;
   const size_t img = (size_t)S1 * S1 * 64;
   const int B2 = 2 * B;
   T.nchunk2 = std::min(B2, 32);

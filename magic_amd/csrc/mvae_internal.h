@@ -83,6 +83,7 @@ struct GemmDesc {
   // diagnostics build of the twin kernel (mvae_bench_gemm, MVAE_STAMPS=1): per workgroup
   // s_memrealtime stamps {start, prologue copy landed, k-loop done, end} (never in the step)
   unsigned long long* stamps = nullptr;
+  int group = -1;                      // bf16 DMA kernels' tile order (Params::group); -1 planner
   GemmEpi epi;
 };
 

@@ -792,15 +792,10 @@ __global__ void mvae_region_marker() {}
 
 hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int* dyn_next,
                                int B, int D, int ldx, int f32mask, int f32dyn_mask, hipStream_t st) {
-  // pixels per thread: 8 (default), 16 or 4 (MVAE_DEINT=16 / 4, A/B); an LDS-staged form with
-  // lane-contiguous loads measured slower (profiles/r4/r4an_deinterleave_lds_rejected.txt)
-  static const int npt = [] { const char* v = std::getenv("MVAE_DEINT"); return v ? std::atoi(v) : 8; }();
+  // 8 pixels per thread (4 and 16 measured slower, profiles/r4/r4y_deinterleave.txt; an LDS-staged
+  // form with lane-contiguous loads too, r4an_deinterleave_lds_rejected.txt); 4 when D % 8 != 0
   const bool al = (reinterpret_cast<uintptr_t>(x) % 16) == 0;
-  if (npt == 16 && (D % 16) == 0 && al && (ldx % 8) == 0) {
-    dim3 g(nblocks(D / 16, 256), B);
-    hipLaunchKernelGGL(deinterleave_vecn_kernel<4>, g, dim3(256), 0, st,
-                       reinterpret_cast<const float4*>(x), xs, xp.p, dyn, B, D, ldx, f32mask, dyn_next);
-  } else if (npt != 4 && (D % 8) == 0 && al && (ldx % 8) == 0) {
+  if ((D % 8) == 0 && al && (ldx % 8) == 0) {
     dim3 g(nblocks(D / 8, 256), B);
     hipLaunchKernelGGL(deinterleave_vecn_kernel<2>, g, dim3(256), 0, st,
                        reinterpret_cast<const float4*>(x), xs, xp.p, dyn, B, D, ldx, f32mask, dyn_next);

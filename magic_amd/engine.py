@@ -58,7 +58,8 @@ class Engine:
         torch.cuda.set_device(device)
         torch.cuda.init()
         h = C.c_void_p()
-        rc = self.lib.mvae_create(C.byref(c), device, C.byref(h))
+        opts = getattr(cfg, "options", "") or None
+        rc = self.lib.mvae_create_ex(C.byref(c), device, opts.encode() if opts else None, C.byref(h))
         if rc != 0:
             raise _lib.MVAEError(rc, (self.lib.mvae_last_error(None) or b"").decode())
         self.ctx = h.value

@@ -89,11 +89,10 @@ def random_shapes(n: int, size: int, gen: torch.Generator, device) -> torch.Tens
 
 
 # areas resampled from the reference's 2a/OVERLAP_AREAS empirical
-# distribution (range 296-6426). tests/golden/overlap_areas.npy holds the 2000 values
-# (extracted without unpickling, tests/golden/make_golden.py); a log-normal fit is the
-# fallback when the fixture is absent.
-_AREAS_FIXTURE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                              "tests", "golden", "overlap_areas.npy")
+# distribution (range 296-6426). magic_amd/data/overlap_areas.npy holds the 2000 values (package
+# data, extracted as text without unpickling by tests/golden/make_golden.py); a log-normal fit is
+# the fallback when the table is absent.
+_AREAS_FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "overlap_areas.npy")
 
 
 def area_distribution() -> np.ndarray:

@@ -28,8 +28,6 @@ split-K, so those rows are not bitwise equal to a single-process one-GEMM backwa
 """
 from __future__ import annotations
 
-import os
-
 import torch
 import torch.distributed as dist
 
@@ -40,7 +38,7 @@ class DataParallelStep:
     CPU stand-in built on the oracle)."""
 
     def __init__(self, engine, group=None, reduce_losses: bool = True, overlap: bool = True,
-                 force_collectives: bool = False, wgrad0_chunks: int = 4):
+                 force_collectives: bool = False, wgrad0_chunks: int = 4, early_adam=None):
         self.e = engine
         # bucketed all-reduce overlapped with the rest of the backward (engines exposing
         # backward_part/grad_ranges); otherwise one bucket after the whole backward
@@ -63,12 +61,12 @@ class DataParallelStep:
             engine.set_option("wgrad0_chunks", wgrad0_chunks)
             self._chunks_set = True
         self._early_set = False
-        early = os.environ.get("MVAE_NO_EARLY_ADAM") != "1" and engine.cfg.precision == "f32x"
+        early = engine.cfg.precision == "f32x" if early_adam is None else bool(early_adam)
         if not self.coll and hasattr(engine, "set_option") and early:
             # no collective between backward() and adam(): Adam of the blocks after layer 0 runs
             # on the engine's side stream beside the layer-0 weight gradient. Measured per mode
             # (profiles/r4/r4ae_early_adam.txt): C2 (f32x) 2.775 -> 2.742 ms, C3 (bf16) 1.992 ->
-            # 2.005 ms, so f32x only; MVAE_NO_EARLY_ADAM=1: one Adam launch after the backward
+            # 2.005 ms, so f32x only by default; early_adam=False: one Adam launch after the backward
             engine.set_option("early_adam", 1)
             self._early_set = True
         elif self.coll and hasattr(engine, "set_option"):

@@ -2,7 +2,8 @@
 """Regenerate the committed fixtures under tests/golden/ (run here, where the read-only
 reference is mounted; the GPU box only reads the committed files).
 
-  overlap_areas.npy      the 2000 int64 labels of the reference's ``2a/OVERLAP_AREAS``
+  magic_amd/data/overlap_areas.npy  the 2000 int64 labels of the reference's ``2a/OVERLAP_AREAS``
+                         (package data: the synthetic batches resample it)
                          (a Python-2 protocol-0 pickle of numpy int64 scalars). The file is
                          NOT unpickled: its ``S'...'`` string literals (8 raw little-endian
                          bytes each) are parsed as text and decoded with escape rules only.
@@ -104,7 +105,7 @@ def main():
     ap.add_argument("--reference", default="/root/reference")
     args = ap.parse_args()
     areas = parse_overlap_areas(os.path.join(args.reference, "2a", "OVERLAP_AREAS"))
-    np.save(os.path.join(HERE, "overlap_areas.npy"), areas)
+    np.save(os.path.join(os.path.dirname(os.path.dirname(HERE)), "magic_amd", "data", "overlap_areas.npy"), areas)
     print("overlap_areas", areas.shape, areas.min(), areas.max(), areas.mean())
     np.savez_compressed(os.path.join(HERE, "overlap_micro.npz"),
                         **pack_micro(os.path.join(args.reference, "overlap_micro.zip")))

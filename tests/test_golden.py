@@ -23,7 +23,7 @@ def load_step(path):
 
 def test_overlap_areas_fixture_matches_reference_statistics():
     """2000 int64 labels, range 296-6426, mean 1972.8, sd 1179.6."""
-    a = np.load(os.path.join(GOLD, "overlap_areas.npy"))
+    a = np.load(os.path.join(os.path.dirname(GOLD), "..", "magic_amd", "data", "overlap_areas.npy"))
     assert a.shape == (2000,) and a.dtype == np.int64
     assert a.min() == 296 and a.max() == 6426
     assert abs(a.mean() - 1972.8) < 0.1 and abs(a.std() - 1179.6) < 1.0

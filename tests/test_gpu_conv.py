@@ -144,7 +144,7 @@ def _conv2_ref(mode, x, y, S1, B):
 @pytest.mark.parametrize("mfma", [0, 1], ids=["valu_f32", "mfma_bf16"])
 @pytest.mark.parametrize("mode", [0, 1, 2], ids=["fwd", "dgrad", "wgrad"])
 @pytest.mark.parametrize("S1,B", [(6, 2), (10, 3), (50, 1)])
-def test_conv2_kernel(mode, mfma, S1, B):
+def test_conv2_kernel(mode, mfma, S1, B, form=0):
     from magic_amd import _lib
     lib = _lib.load()
     rng = np.random.default_rng(S1 * 10 + mode)
@@ -158,7 +158,7 @@ def test_conv2_kernel(mode, mfma, S1, B):
         y = (rng.standard_normal(1601 * 64) * 0.05).astype(np.float32)
         out = torch.zeros((3 * B if mode == 0 else 4 * B) * img, device="cuda")
     xd, yd = to_dev(x), to_dev(y)
-    rc = lib.mvae_debug_conv2(S1, B, mode, mfma, xd.data_ptr(), yd.data_ptr(), out.data_ptr(),
+    rc = lib.mvae_debug_conv2(S1, B, mode, mfma | form, xd.data_ptr(), yd.data_ptr(), out.data_ptr(),
                               torch.cuda.current_stream().cuda_stream)
     assert rc == 0, lib.mvae_last_error(None)
     xr, yr = (_bf16(x), _bf16(y)) if mfma else (x, y)
@@ -171,9 +171,8 @@ def test_conv2_kernel(mode, mfma, S1, B):
 
 
 @pytest.mark.parametrize("mode", [0, 1], ids=["fwd", "dgrad"])
-def test_conv2_kernel_full_channel_form(mode, monkeypatch):
-    """The full-channel forward / data-gradient kernel (MVAE_CONV2_HALF=0; the default is the
-    channel-half form) to the same bound."""
-    monkeypatch.setenv("MVAE_CONV2_HALF", "0")
-    test_conv2_kernel(mode, 1, 50, 1)
+def test_conv2_kernel_full_channel_form(mode):
+    """The full-channel forward / data-gradient kernel (mvae_debug_conv2 form bit 1, the create
+    option conv2_half=0; the default is the channel-half form) to the same bound."""
+    test_conv2_kernel(mode, 1, 50, 1, form=2)
 

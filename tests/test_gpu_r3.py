@@ -1,6 +1,6 @@
 """GPU parity for the eight-phase 256x256 GEMM kernel (gemm_bf16e.hip, round 4) on every
 operand layout, ragged edge and fused epilogue, and whole training steps with it forced onto
-every 256-row bf16 DMA GEMM (MVAE_E8=2) or excluded (MVAE_E8=0), against the float64 oracle at
+every 256-row bf16 DMA GEMM (create option e8=2) or excluded (e8=0), against the float64 oracle at
 the fp32 bar (f32x) and the documented bf16 bar; plus the round-3 items (chunked layer-0
 gradient, 192-row ring tiles, latent sampling grid)."""
 import pytest
@@ -93,12 +93,12 @@ def test_gemm_e8_epilogues(prec, epi, act, M, N, ldc, variant, planes):
 @pytest.mark.parametrize("mode", ["0", "2"], ids=["ring_only", "e8_everywhere"])
 @pytest.mark.parametrize("prec", ["f32x", "bf16"])
 @pytest.mark.parametrize("grey", [False, True], ids=["binary", "grey"])
-def test_step_e8_modes(monkeypatch, mode, prec, grey):
+def test_step_e8_modes(mode, prec, grey):
     """A whole step with every 256-row bf16 DMA GEMM on the eight-phase kernel (BCE head with fp32
     or bf16-plane target, DACT row remap, batch-2 weight gradients, split-K) or on the ring
     kernels only."""
-    monkeypatch.setenv("MVAE_E8", mode)
-    cfg = preset("8c", image_size=20, batch=288, precision=prec).replace(enc=(300, 260, 280))
+    cfg = preset("8c", image_size=20, batch=288, precision=prec).replace(enc=(300, 260, 280),
+                                                                        options=f"e8={mode}")
     if prec == "f32x":
         check_step(cfg, grey=grey, recon=True)
     else:
@@ -106,18 +106,16 @@ def test_step_e8_modes(monkeypatch, mode, prec, grey):
 
 
 @pytest.mark.parametrize("mode", ["1", "2"], ids=["planner", "e8_everywhere"])
-def test_step_c3_shape_e8(monkeypatch, mode):
+def test_step_c3_shape_e8(mode):
     """BASELINE C3's shapes (8d, bf16, 100x100, enc [500]*4, L = 200) at B = 2048 with the default
     plan and with the eight-phase kernel everywhere, documented bf16 bar."""
-    monkeypatch.setenv("MVAE_E8", mode)
-    check_step(baseline_config("C3").replace(batch=2048), adam=False, **BF16)
+    check_step(baseline_config("C3").replace(batch=2048, options=f"e8={mode}"), adam=False, **BF16)
 
 
-def test_step_c2_f32x_e8_everywhere(monkeypatch):
+def test_step_c2_f32x_e8_everywhere():
     """The benched C2 configuration (f32x, B = 4096) with the eight-phase kernel on every 256-row
     bf16 GEMM, at the fp32 bar."""
-    monkeypatch.setenv("MVAE_E8", "2")
-    check_step(preset("8c", image_size=100, batch=4096, precision="f32x"), adam=False)
+    check_step(preset("8c", image_size=100, batch=4096, precision="f32x", options="e8=2"), adam=False)
 
 
 # ------------------------------------------------------------------ chunked layer-0 gradient

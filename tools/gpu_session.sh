@@ -1,16 +1,14 @@
 #!/bin/bash
 # The current GPU session (overwritten per session; earlier sessions are in git history):
 #   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r5e: why the library's eight-phase k-loop runs ~3300 cycles per k-tile where the template runs
-# ~2430 on the same NT 4096^3 shape: tile-group order (template --gm 4 / 8; library
-# MVAE_TILE_GROUP 0 / 4 / 8), stamped library k-loop without DMA (diag 1) / without fragment reads
-# (diag 64) / without both.
+# r5g: (1) k-loop time per k-tile of the template and the library's eight-phase kernel without
+# stamps: the same M x N at K = 4096, 8192, 16384 (the K difference cancels prologue/epilogue);
+# (2) the tests touched by the create-option refactor (no environment switches in the library).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-S="MVAE_STAMPS=2 python tools/gemm_bench.py --variants 29 --rounds 1 --config C3 --shapes square4096"
+T="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
 bash tools/gpu_steps.sh \
-  "r5e_t4|120|tools/micro/gemm8p 4096 4096 4096 --rounds 3 --gm 4 --lib magic_amd/libmvae.so" \
-  "r5e_t8|120|tools/micro/gemm8p 4096 4096 4096 --rounds 3 --gm 8 --lib magic_amd/libmvae.so" \
-  "r5e_l4|120|MVAE_TILE_GROUP=4 tools/micro/gemm8p 4096 4096 4096 --rounds 3 --gm 4 --lib magic_amd/libmvae.so" \
-  "r5e_l0|120|MVAE_TILE_GROUP=0 tools/micro/gemm8p 4096 4096 4096 --rounds 3 --gm 4 --lib magic_amd/libmvae.so" \
-  "r5e_sd|200|$S --diag 0,1,64,65,128" \
-  "r5e_sd4|200|MVAE_TILE_GROUP=4 $S --diag 0,1" 
+  "r5g_k4|120|tools/micro/gemm8p 4096 4096 4096 --rounds 5 --lib magic_amd/libmvae.so" \
+  "r5g_k8|120|tools/micro/gemm8p 4096 4096 8192 --rounds 5 --lib magic_amd/libmvae.so" \
+  "r5g_k16|120|tools/micro/gemm8p 4096 4096 16384 --rounds 5 --lib magic_amd/libmvae.so" \
+  "r5g_tests|600|$T tests/test_gpu_r3.py tests/test_gpu_conv.py tests/test_gpu_dp.py tests/test_input_pipeline.py" \
+  "r5g_smoke|300|python -c 'import __graft_entry__ as g; g.smoke()'"
