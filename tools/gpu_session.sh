@@ -1,14 +1,14 @@
 #!/bin/bash
 # The current GPU session (overwritten per session; earlier sessions are in git history):
 #   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r5g: (1) k-loop time per k-tile of the template and the library's eight-phase kernel without
-# stamps: the same M x N at K = 4096, 8192, 16384 (the K difference cancels prologue/epilogue);
-# (2) the tests touched by the create-option refactor (no environment switches in the library).
+# r5i: the planner's ring-fill rule (single-product GEMMs whose 192-row ring tiles fill one round
+# stay on the ring kernel) against the rebuilt eight-phase kernel: default vs libmvae_norf.so (the
+# rule off: the layer-0 and hidden forwards on the eight-phase kernel), alternating, C3 / C5 / C2.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-T="python -u -m pytest -x -q --timeout 300 --timeout-method thread -p no:cacheprovider"
+BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 40"
+NR=MVAE_LIB=magic_amd/libmvae_norf.so
+r() { echo "r5i_$1|120|$3 python bench.py --config $2 $BQ > gpurun_out/r5i_$1.json"; }
 bash tools/gpu_steps.sh \
-  "r5g_k4|120|tools/micro/gemm8p 4096 4096 4096 --rounds 5 --lib magic_amd/libmvae.so" \
-  "r5g_k8|120|tools/micro/gemm8p 4096 4096 8192 --rounds 5 --lib magic_amd/libmvae.so" \
-  "r5g_k16|120|tools/micro/gemm8p 4096 4096 16384 --rounds 5 --lib magic_amd/libmvae.so" \
-  "r5g_tests|600|$T tests/test_gpu_r3.py tests/test_gpu_conv.py tests/test_gpu_dp.py tests/test_input_pipeline.py" \
-  "r5g_smoke|300|python -c 'import __graft_entry__ as g; g.smoke()'"
+  "$(r c3_d1 C3)" "$(r c3_n1 C3 $NR)" "$(r c3_d2 C3)" "$(r c3_n2 C3 $NR)" \
+  "$(r c5_d1 C5)" "$(r c5_n1 C5 $NR)" "$(r c5_d2 C5)" "$(r c5_n2 C5 $NR)" \
+  "$(r c2_d1 C2)" "$(r c2_n1 C2 $NR)" "$(r c2_d2 C2)" "$(r c2_n2 C2 $NR)"
