@@ -127,7 +127,8 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out);
  * 0 ring kernels only, 2 the eight-phase kernel wherever a 256-row kernel runs), thin_ring (0-2),
  * valu (0/1), dact_planes (0/1), bce_split (0/1), plan_log (0/1: GEMM plans on stderr),
  * conv2_half (0/1), conv2_nw (4/8/16), conv2_tpb (1/2), conv2_fpw (2/4), conv2_wg (4/8),
- * conv2_nchunk (> 0). An unknown name or a value out of range is MVAE_EINVAL. The library reads
+ * conv2_nchunk (> 0); diag_skip_deint (1: de-interleave only the first batch -- a timing bound,
+ * results meaningless). An unknown name or a value out of range is MVAE_EINVAL. The library reads
  * no environment variables (the diagnostics entry point mvae_bench_gemm aside). */
 int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ctx** out);
 int mvae_destroy(mvae_ctx* ctx);

@@ -40,6 +40,16 @@ constexpr uint64_t EVAL_STREAM = 1ull << 63;
 struct mvae_ctx {
   mvae_cfg cfg{};
   int device = 0;
+  bool diag_skip_deint = false;  // create option diag_skip_deint (timing bound only: wrong results)
+  int adam_side_grid = 0;        // option "adam_side_grid": the early Adam's workgroups (0: one per 256 elements)
+  // diagnostics (create options diag_shadow_deint / diag_shadow_at): a second de-interleave of
+  // the step's input into a scratch image on a low-priority stream beside the step -- the cost
+  // to the step of staging the next batch's pass (grid: -1 the normal launch, > 0 persistent)
+  int diag_shadow = 0, diag_shadow_at = 0;
+  hipStream_t stage = nullptr;
+  bool stage_pending = false;
+  unsigned short* shadow = nullptr;
+  const float* last_x = nullptr;
   int B = 0, D = 0, L = 0, nenc = 0, d0 = 0, d1 = 0;
   float inv_bg = 1.f;
   int ldx = 0, ldz = 0, ld_d1 = 0, ld_d2 = 0, ld_u = 0, lddz = 0, ld_dh = 0, nblk = 0, nchunk = 0;
@@ -388,6 +398,7 @@ int mvae_destroy(mvae_ctx* ctx) {
   for (auto e : ctx->event_pool) hipEventDestroy(e);
   for (auto e : ctx->sync_ev) hipEventDestroy(e);
   if (ctx->side) hipStreamDestroy(ctx->side);
+  if (ctx->stage) hipStreamDestroy(ctx->stage);
   for (void* p : ctx->allocs) hipFree(p);
   hipSetDevice(dev);
   delete ctx;
@@ -405,6 +416,9 @@ struct CreateOpts {
   int dact_planes = 1;  // bf16 mode: DACT epilogues read the activation's bf16 plane
   int bce_split = 1;    // the BCE head in whole rounds + 256x128 ring tiles
   int plan_log = 0;     // print the GEMM plans on stderr
+  int diag_skip_deint = 0;  // diagnostics: de-interleave only the first batch (the step's time
+                            // without its streaming pass; results meaningless)
+  int diag_shadow_deint = 0, diag_shadow_at = 0;  // diagnostics: see mvae_ctx::diag_shadow
   int conv2_nw = 8, conv2_tpb = 1, conv2_fpw = 2, conv2_wg = 8, conv2_half = 1, conv2_nchunk = 0;
 };
 
@@ -431,6 +445,9 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "dact_planes" && in(0, 1)) o->dact_planes = (int)v;
     else if (k == "bce_split" && in(0, 1)) o->bce_split = (int)v;
     else if (k == "plan_log" && in(0, 1)) o->plan_log = (int)v;
+    else if (k == "diag_skip_deint" && in(0, 1)) o->diag_skip_deint = (int)v;
+    else if (k == "diag_shadow_deint" && in(-1, 1 << 16)) o->diag_shadow_deint = (int)v;
+    else if (k == "diag_shadow_at" && in(0, 2)) o->diag_shadow_at = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
     else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
     else if (k == "conv2_fpw" && (v == 2 || v == 4)) o->conv2_fpw = (int)v;
@@ -457,6 +474,9 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
   if (!ctx) return fail(nullptr, MVAE_EINVAL, "out of host memory");
   ctx->cfg = *cfg;
   ctx->device = device;
+  ctx->diag_skip_deint = opt.diag_skip_deint != 0;
+  ctx->diag_shadow = opt.diag_shadow_deint;
+  ctx->diag_shadow_at = opt.diag_shadow_at;
   hipError_t he = hipSetDevice(device);
   if (he != hipSuccess) { g_create_err = hipGetErrorString(he); delete ctx; return (int)he; }
   auto c = ctx;
@@ -838,6 +858,12 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
     int lo = 0, hi = 0;
     hipError_t se = hipDeviceGetStreamPriorityRange(&lo, &hi);
     if (se == hipSuccess) se = hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, lo);
+    if (se == hipSuccess && c->diag_shadow) {
+      se = hipStreamCreateWithPriority(&c->stage, hipStreamNonBlocking, lo);
+      void* q = nullptr;
+      if (se == hipSuccess) se = hipMalloc(&q, (size_t)3 * c->B * c->ldx * sizeof(unsigned short));
+      if (se == hipSuccess) { c->allocs.push_back(q); c->shadow = static_cast<unsigned short*>(q); }
+    }
     for (int i = 0; se == hipSuccess && i < 16; ++i) {
       hipEvent_t ev = nullptr;
       se = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
@@ -1036,9 +1062,17 @@ static int stream_wait(mvae_ctx* ctx, hipStream_t from, hipStream_t to) {
 // latent mean/log-sigma heads only (transform: no eps, no z, no column statistics).
 enum { ENC_TRAIN = 0, ENC_EVAL = 1, ENC_MEAN = 2 };
 
+static int shadow_deint(mvae_ctx* ctx, hipStream_t st);
+
 static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t st, int draw = ENC_TRAIN) {
   auto c = ctx;
-  {
+  c->last_x = x;
+  if (c->stage_pending) {  // (diagnostics) the last shadow pass ends before this step
+    c->stage_pending = false;
+    MV_CHECK(hipEventRecord(c->sync_ev[c->sync_next % c->sync_ev.size()], c->stage));
+    MV_CHECK(hipStreamWaitEvent(st, c->sync_ev[c->sync_next++ % c->sync_ev.size()], 0));
+  }
+  if (!(c->diag_skip_deint && c->dyn_cur)) {  // (diagnostics: the stale image of the last pass)
     TIMED("deinterleave");
     // the flag's slots alternate: this pass raises the one the previous pass zeroed and zeroes
     // the previous one (its readers are all behind on this stream), no memset launch per step
@@ -1047,6 +1081,10 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
     MV_CHECK(launch_deinterleave(x, c->xs, planes_of(c, c->xs), cur, c->dyn ? prev : nullptr, c->B,
                                  c->D, c->ldx, c->x32mask, c->x32dyn, st));
     c->dyn_cur = cur;
+  }
+  if (c->diag_shadow && c->diag_shadow_at == 0 && draw == ENC_TRAIN) {
+    int rc = shadow_deint(c, st);
+    if (rc) return rc;
   }
   const size_t ne = (size_t)3 * c->B * c->L;
   if (draw != ENC_MEAN) {
@@ -1157,9 +1195,22 @@ extern "C" int mvae_metric(mvae_ctx* ctx, const float* areas, void* stream) {
 static int w0n(const mvae_ctx* c) { return c->w0_chunks == 1 ? 1 : (int)c->w0c[c->w0_chunks].size(); }
 static int nparts(const mvae_ctx* c) { return w0n(c) + 2; }
 
+// (diagnostics) the shadow de-interleave on the stage stream, after the work on st so far
+static int shadow_deint(mvae_ctx* ctx, hipStream_t st) {
+  auto c = ctx;
+  if (!c->last_x || !c->stage) return MVAE_OK;
+  MV_CHECK(hipEventRecord(c->sync_ev[c->sync_next % c->sync_ev.size()], st));
+  MV_CHECK(hipStreamWaitEvent(c->stage, c->sync_ev[c->sync_next++ % c->sync_ev.size()], 0));
+  MV_CHECK(launch_deinterleave_grid(c->last_x, c->shadow, c->B, c->D, c->ldx, c->diag_shadow, c->stage));
+  c->stage_pending = true;
+  return MVAE_OK;
+}
+
 static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec) {
   auto c = ctx;
   int rc;
+  if (c->diag_shadow && part == 0 && c->diag_shadow_at == 1 && (rc = shadow_deint(c, st))) return rc;
+  if (c->diag_shadow && part == 1 && c->diag_shadow_at == 2 && (rc = shadow_deint(c, st))) return rc;
   const int R = w0n(c);
   const bool two = c->use_side && c->side;
   hipStream_t sd = two ? c->side : st;
@@ -1302,6 +1353,11 @@ extern "C" int mvae_set_option(mvae_ctx* ctx, const char* name, int value) {
     ctx->early_adam = value != 0;
     return MVAE_OK;
   }
+  if (k == "adam_side_grid") {
+    if (value < 0 || value > 65535) return fail(ctx, MVAE_EINVAL, "adam_side_grid must be in [0, 65535]");
+    ctx->adam_side_grid = value;
+    return MVAE_OK;
+  }
   if (k == "wgrad0_chunks") {
     if (value != 1 && value != 2 && value != 4 && value != 8)
       return fail(ctx, MVAE_EINVAL, "wgrad0_chunks must be 1, 2, 4 or 8");
@@ -1366,6 +1422,7 @@ extern "C" int mvae_adam(mvae_ctx* ctx, void* stream) {
     AdamArgs a1 = a, a0 = a;
     a1.i0 = l1;
     a0.i1 = l1;
+    a1.grid = c->adam_side_grid;  // capped grid (option "adam_side_grid"; 0: one thread per element)
     MV_CHECK(launch_adam(a1, c->side));
     {
       TIMED("adam");

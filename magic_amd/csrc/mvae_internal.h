@@ -125,6 +125,10 @@ struct Planes {
 // whose last readers ran before it on the stream.
 hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int* dyn_next,
                                int B, int D, int ldx, int f32mask, int f32dyn_mask, hipStream_t st);
+// (diagnostics) the bf16 plane-0 pass alone into xp: grid -1 the normal launch, > 0 that many
+// persistent 256-thread workgroups striding over the rows' 8-pixel groups
+hipError_t launch_deinterleave_grid(const float* x, unsigned short* xp, int B, int D, int ldx, int grid,
+                                    hipStream_t st);
 // N(0,1) into out[slots][B][L]: elements (s*Bg + off + b)*L + l of the counter's global stream
 // (Bg rows per slot over all ranks, this rank's rows starting at off)
 hipError_t launch_normal(float* out, int slots, int B, int L, int Bg, int off, uint64_t seed,
@@ -159,6 +163,7 @@ struct AdamArgs {
   size_t n_all, n_enc; float lr1, lr2, b1, b2, eps;
   Planes tp;  // bf16 plane image of theta refreshed in the same pass (bf16 / f32x modes)
   size_t i0 = 0, i1 = ~size_t(0);  // the index range [i0, min(i1, n_all)) this launch updates
+  int grid = 0;  // > 0: 4 elements per thread in a grid-stride loop over this many workgroups
 };
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
 hipError_t launch_split_planes(const float* src, size_t n, const Planes& dst, hipStream_t st);

@@ -151,6 +151,21 @@ __global__ void deinterleave_vecn_kernel(const float4* __restrict__ x, float* __
   if (dyn && __ballot(nz) != 0 && (threadIdx.x & 63) == 0) atomicOr(dyn, 1);
 }
 
+// (diagnostics) persistent form: gridDim.x workgroups stride over the B x D/8 pixel groups
+__global__ void deinterleave_persist_kernel(const float4* __restrict__ x, unsigned short* __restrict__ xp,
+                                            int B, int D, int ldx) {
+  const int nq = D / 8;
+  const size_t n = (size_t)B * nq;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(i / nq), q = (int)(i % nq);
+    const float4* src = x + ((size_t)b * 3 * D) / 4 + 6 * (size_t)q;
+    float4 v[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v[k] = src[k];
+    deint_put<2>(v, nullptr, xp, B, b, (size_t)8 * q, ldx, 0);
+  }
+}
+
 __global__ void deinterleave_scalar_kernel(const float* __restrict__ x, float* __restrict__ xs,
                                            unsigned short* __restrict__ xp, int* __restrict__ dyn,
                                            int B, int D, int ldx, int f32mask, int* __restrict__ dyn_next) {
@@ -679,6 +694,36 @@ __global__ void adam_kernel(AdamArgs a) {
   if (a.tp.p) planes_put(a.tp.p, a.tp.stride, a.tp.n, i, th);
 }
 
+// the same update, 4 elements per thread (16-B accesses) in a grid-stride loop over a capped grid:
+// the side stream's Adam beside the layer-0 weight gradient, leaving most CU slots to the GEMM
+// (i0, i1, n_enc multiples of 4: blocks start on 64-float boundaries)
+__global__ void adam4_kernel(AdamArgs a) {
+  const size_t n4 = (a.i1 - a.i0) / 4;
+  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (size_t)gridDim.x * blockDim.x) {
+    const size_t i = a.i0 + 4 * q;
+    float4 th = *reinterpret_cast<const float4*>(a.theta + i);
+    float t[4] = {th.x, th.y, th.z, th.w};
+    auto upd = [&](const float* gp, float* mp, float* vp, float lr) {
+      const float4 g = *reinterpret_cast<const float4*>(gp + i);
+      float4 m = *reinterpret_cast<const float4*>(mp + i), v = *reinterpret_cast<const float4*>(vp + i);
+      const float gg[4] = {g.x, g.y, g.z, g.w};
+      float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        mm[j] += (gg[j] - mm[j]) * (1.f - a.b1);
+        vv[j] += (gg[j] * gg[j] - vv[j]) * (1.f - a.b2);
+        t[j] -= (lr * mm[j]) / (sqrtf(vv[j]) + a.eps);
+      }
+      *reinterpret_cast<float4*>(mp + i) = make_float4(mm[0], mm[1], mm[2], mm[3]);
+      *reinterpret_cast<float4*>(vp + i) = make_float4(vv[0], vv[1], vv[2], vv[3]);
+    };
+    upd(a.g1, a.m1, a.v1, a.lr1);
+    if (i < a.n_enc) upd(a.g2, a.m2, a.v2, a.lr2);
+    *reinterpret_cast<float4*>(a.theta + i) = make_float4(t[0], t[1], t[2], t[3]);
+    if (a.tp.p) planes_put4(a.tp.p, a.tp.stride, a.tp.n, i, t);
+  }
+}
+
 __global__ void split_planes_kernel(const float* __restrict__ s, size_t n, unsigned short* p,
                                     long long ps, int np) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -815,6 +860,20 @@ hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int*
   return hipGetLastError();
 }
 
+hipError_t launch_deinterleave_grid(const float* x, unsigned short* xp, int B, int D, int ldx, int grid,
+                                    hipStream_t st) {
+  if ((D % 8) || (ldx % 8) || (reinterpret_cast<uintptr_t>(x) % 16)) return hipErrorInvalidValue;
+  if (grid < 0) {
+    dim3 g(nblocks(D / 8, 256), B);
+    hipLaunchKernelGGL(deinterleave_vecn_kernel<2>, g, dim3(256), 0, st, reinterpret_cast<const float4*>(x),
+                       nullptr, xp, nullptr, B, D, ldx, 0, nullptr);
+  } else if (grid > 0) {
+    hipLaunchKernelGGL(deinterleave_persist_kernel, dim3(grid), dim3(256), 0, st,
+                       reinterpret_cast<const float4*>(x), xp, B, D, ldx);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_normal(float* out, int slots, int B, int L, int Bg, int off, uint64_t seed,
                          uint64_t counter, hipStream_t st) {
   const size_t n = (size_t)B * L;
@@ -896,6 +955,10 @@ hipError_t launch_adam(const AdamArgs& a, hipStream_t st) {
   AdamArgs r = a;
   r.i1 = a.i1 < a.n_all ? a.i1 : a.n_all;
   if (r.i0 >= r.i1) return hipSuccess;
+  if (a.grid > 0 && (r.i0 % 4) == 0 && (r.i1 % 4) == 0 && (r.n_enc % 4) == 0) {
+    hipLaunchKernelGGL(adam4_kernel, dim3(a.grid), dim3(256), 0, st, r);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(adam_kernel, dim3(nblocks(r.i1 - r.i0, 256)), dim3(256), 0, st, r);
   return hipGetLastError();
 }
