@@ -127,9 +127,12 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out);
  * 0 ring kernels only, 2 the eight-phase kernel wherever a 256-row kernel runs), thin_ring (0-2),
  * valu (0/1), dact_planes (0/1), bce_split (0/1), plan_log (0/1: GEMM plans on stderr),
  * conv2_half (0/1), conv2_nw (4/8/16), conv2_tpb (1/2), conv2_fpw (2/4), conv2_wg (4/8),
- * conv2_nchunk (> 0); diag_skip_deint (1: de-interleave only the first batch -- a timing bound,
- * results meaningless). An unknown name or a value out of range is MVAE_EINVAL. The library reads
- * no environment variables (the diagnostics entry point mvae_bench_gemm aside). */
+ * conv2_nchunk (> 0); diagnostics, results meaningless: diag_skip_deint (1: de-interleave only
+ * the first batch -- a timing bound), diag_shadow_deint (-1 or a workgroup count > 0: a second
+ * de-interleave of each step's input into a scratch image on a low-priority stream, launched at
+ * diag_shadow_at = 0 the forward, 1 the backward, 2 the encoder backward -- the cost of staging).
+ * An unknown name or a value out of range is MVAE_EINVAL. The library reads no environment
+ * variables (the diagnostics entry point mvae_bench_gemm aside). */
 int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ctx** out);
 int mvae_destroy(mvae_ctx* ctx);
 const char* mvae_last_error(mvae_ctx* ctx);   /* ctx may be NULL (creation errors) */
@@ -180,7 +183,7 @@ int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* cou
  * lets mvae_adam update the blocks after the layer-0 block on the side stream as soon as the
  * backward has written their gradients (beside the layer-0 weight gradient): only for callers
  * that do not modify MVAE_BUF_GRADS between mvae_backward and mvae_adam (no all-reduce);
- * mvae_train_step uses it in the f32x mode; "bce_split" (default 1) runs a BCE head whose
+ * mvae_train_step uses it in the bf16 and f32x modes; "bce_split" (default 1) runs a BCE head whose
  * 256x256 tiles leave a partial last round as the whole rounds plus 256x128 tiles for the rest
  * (the same results). */
 int mvae_set_option(mvae_ctx* ctx, const char* name, int value);

@@ -41,7 +41,6 @@ struct mvae_ctx {
   mvae_cfg cfg{};
   int device = 0;
   bool diag_skip_deint = false;  // create option diag_skip_deint (timing bound only: wrong results)
-  int adam_side_grid = 0;        // option "adam_side_grid": the early Adam's workgroups (0: one per 256 elements)
   // diagnostics (create options diag_shadow_deint / diag_shadow_at): a second de-interleave of
   // the step's input into a scratch image on a low-priority stream beside the step -- the cost
   // to the step of staging the next batch's pass (grid: -1 the normal launch, > 0 persistent)
@@ -1353,11 +1352,6 @@ extern "C" int mvae_set_option(mvae_ctx* ctx, const char* name, int value) {
     ctx->early_adam = value != 0;
     return MVAE_OK;
   }
-  if (k == "adam_side_grid") {
-    if (value < 0 || value > 65535) return fail(ctx, MVAE_EINVAL, "adam_side_grid must be in [0, 65535]");
-    ctx->adam_side_grid = value;
-    return MVAE_OK;
-  }
   if (k == "wgrad0_chunks") {
     if (value != 1 && value != 2 && value != 4 && value != 8)
       return fail(ctx, MVAE_EINVAL, "wgrad0_chunks must be 1, 2, 4 or 8");
@@ -1422,7 +1416,6 @@ extern "C" int mvae_adam(mvae_ctx* ctx, void* stream) {
     AdamArgs a1 = a, a0 = a;
     a1.i0 = l1;
     a0.i1 = l1;
-    a1.grid = c->adam_side_grid;  // capped grid (option "adam_side_grid"; 0: one thread per element)
     MV_CHECK(launch_adam(a1, c->side));
     {
       TIMED("adam");
@@ -1449,10 +1442,10 @@ extern "C" int mvae_train_step(mvae_ctx* ctx, const float* x, const float* areas
   if (losses_out) MV_CHECK(hipMemcpyAsync(losses_out, ctx->losses, 5 * sizeof(float), hipMemcpyDeviceToDevice, st));
   if (dist_out) MV_CHECK(hipMemcpyAsync(dist_out, ctx->dist, ctx->B * sizeof(float), hipMemcpyDeviceToDevice, st));
   // nothing touches the gradients between the two: Adam of the blocks after layer 0 may run
-  // beside the layer-0 weight gradient (option "early_adam"; measured faster in the f32x mode
-  // only, profiles/r4/r4ae_early_adam.txt)
+  // beside the layer-0 weight gradient (option "early_adam"; f32x since profiles/r4/
+  // r4ae_early_adam.txt, bf16 since the round-5 kernels: C3 1.837 vs 1.844 ms, r5m / r5n)
   const bool ea = ctx->early_adam;
-  ctx->early_adam = ea || ctx->np == 3;
+  ctx->early_adam = ea || ctx->np != 0;
   rc = mvae_backward(ctx, stream);
   ctx->early_adam = ea;
   if (rc) return rc;

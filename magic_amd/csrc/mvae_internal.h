@@ -163,7 +163,6 @@ struct AdamArgs {
   size_t n_all, n_enc; float lr1, lr2, b1, b2, eps;
   Planes tp;  // bf16 plane image of theta refreshed in the same pass (bf16 / f32x modes)
   size_t i0 = 0, i1 = ~size_t(0);  // the index range [i0, min(i1, n_all)) this launch updates
-  int grid = 0;  // > 0: 4 elements per thread in a grid-stride loop over this many workgroups
 };
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
 hipError_t launch_split_planes(const float* src, size_t n, const Planes& dst, hipStream_t st);

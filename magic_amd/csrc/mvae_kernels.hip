@@ -694,36 +694,6 @@ __global__ void adam_kernel(AdamArgs a) {
   if (a.tp.p) planes_put(a.tp.p, a.tp.stride, a.tp.n, i, th);
 }
 
-// the same update, 4 elements per thread (16-B accesses) in a grid-stride loop over a capped grid:
-// the side stream's Adam beside the layer-0 weight gradient, leaving most CU slots to the GEMM
-// (i0, i1, n_enc multiples of 4: blocks start on 64-float boundaries)
-__global__ void adam4_kernel(AdamArgs a) {
-  const size_t n4 = (a.i1 - a.i0) / 4;
-  for (size_t q = (size_t)blockIdx.x * blockDim.x + threadIdx.x; q < n4; q += (size_t)gridDim.x * blockDim.x) {
-    const size_t i = a.i0 + 4 * q;
-    float4 th = *reinterpret_cast<const float4*>(a.theta + i);
-    float t[4] = {th.x, th.y, th.z, th.w};
-    auto upd = [&](const float* gp, float* mp, float* vp, float lr) {
-      const float4 g = *reinterpret_cast<const float4*>(gp + i);
-      float4 m = *reinterpret_cast<const float4*>(mp + i), v = *reinterpret_cast<const float4*>(vp + i);
-      const float gg[4] = {g.x, g.y, g.z, g.w};
-      float mm[4] = {m.x, m.y, m.z, m.w}, vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        mm[j] += (gg[j] - mm[j]) * (1.f - a.b1);
-        vv[j] += (gg[j] * gg[j] - vv[j]) * (1.f - a.b2);
-        t[j] -= (lr * mm[j]) / (sqrtf(vv[j]) + a.eps);
-      }
-      *reinterpret_cast<float4*>(mp + i) = make_float4(mm[0], mm[1], mm[2], mm[3]);
-      *reinterpret_cast<float4*>(vp + i) = make_float4(vv[0], vv[1], vv[2], vv[3]);
-    };
-    upd(a.g1, a.m1, a.v1, a.lr1);
-    if (i < a.n_enc) upd(a.g2, a.m2, a.v2, a.lr2);
-    *reinterpret_cast<float4*>(a.theta + i) = make_float4(t[0], t[1], t[2], t[3]);
-    if (a.tp.p) planes_put4(a.tp.p, a.tp.stride, a.tp.n, i, t);
-  }
-}
-
 __global__ void split_planes_kernel(const float* __restrict__ s, size_t n, unsigned short* p,
                                     long long ps, int np) {
   const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -955,10 +925,6 @@ hipError_t launch_adam(const AdamArgs& a, hipStream_t st) {
   AdamArgs r = a;
   r.i1 = a.i1 < a.n_all ? a.i1 : a.n_all;
   if (r.i0 >= r.i1) return hipSuccess;
-  if (a.grid > 0 && (r.i0 % 4) == 0 && (r.i1 % 4) == 0 && (r.n_enc % 4) == 0) {
-    hipLaunchKernelGGL(adam4_kernel, dim3(a.grid), dim3(256), 0, st, r);
-    return hipGetLastError();
-  }
   hipLaunchKernelGGL(adam_kernel, dim3(nblocks(r.i1 - r.i0, 256)), dim3(256), 0, st, r);
   return hipGetLastError();
 }

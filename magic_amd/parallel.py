@@ -61,12 +61,14 @@ class DataParallelStep:
             engine.set_option("wgrad0_chunks", wgrad0_chunks)
             self._chunks_set = True
         self._early_set = False
-        early = engine.cfg.precision == "f32x" if early_adam is None else bool(early_adam)
+        early = engine.cfg.precision in ("f32x", "bf16") if early_adam is None else bool(early_adam)
         if not self.coll and hasattr(engine, "set_option") and early:
             # no collective between backward() and adam(): Adam of the blocks after layer 0 runs
-            # on the engine's side stream beside the layer-0 weight gradient. Measured per mode
-            # (profiles/r4/r4ae_early_adam.txt): C2 (f32x) 2.775 -> 2.742 ms, C3 (bf16) 1.992 ->
-            # 2.005 ms, so f32x only by default; early_adam=False: one Adam launch after the backward
+            # on the engine's side stream beside the layer-0 weight gradient. Measured per mode:
+            # C2 (f32x) 2.775 -> 2.742 ms (profiles/r4/r4ae_early_adam.txt); C3 (bf16) slower
+            # with round 4's kernels (1.992 -> 2.005 ms), faster with round 5's (1.844 -> 1.837 ms
+            # over 4 same-box pairs, profiles/r5/r5n_early_adam_bf16.txt); early_adam=False: one
+            # Adam launch after the backward
             engine.set_option("early_adam", 1)
             self._early_set = True
         elif self.coll and hasattr(engine, "set_option"):

@@ -311,19 +311,16 @@ def test_side_stream_schedule_is_bitwise_identical(prec):
 def test_early_adam_is_bitwise_identical(prec):
     """Option early_adam (Adam of the blocks after layer 0 on the side stream, beside the layer-0
     weight gradient) vs one Adam launch after the backward, and mvae_train_step (which uses it
-    in the f32x mode), and the early Adam on a capped grid of float4 grid-stride workgroups
-    (option adam_side_grid): bitwise identical parameters after three steps."""
+    in the plane modes): bitwise identical parameters after three steps."""
     cfg = preset("8c", image_size=40, batch=768, precision=prec).replace(enc=(400, 300, 260))
     P = make_params(cfg)
     X, areas, eps = make_inputs(cfg, cfg.batch)
     x, a, e = to_dev(X), to_dev(areas), to_dev(eps)
     outs = []
-    for mode in ("early", "late", "train_step", "early_capped"):
+    for mode in ("early", "late", "train_step"):
         eng = _engine(cfg)  # fresh Adam state per mode
         try:
-            eng.set_option("early_adam", 1 if mode.startswith("early") else 0)
-            if mode == "early_capped":
-                eng.set_option("adam_side_grid", 64)
+            eng.set_option("early_adam", 1 if mode == "early" else 0)
             eng.load_params(P)
             for _ in range(3):
                 if mode == "train_step":

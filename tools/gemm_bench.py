@@ -57,6 +57,8 @@ def main():
     ap.add_argument("--epilogues", action="store_true", help="run each shape with its step epilogue")
     ap.add_argument("--diag", default="0", help="kernel diagnostics bits (PParams::diag), comma list")
     ap.add_argument("--shapes", default="", help="comma list of shape names (default: all)")
+    ap.add_argument("--extra", action="append", default=[],
+                    help="extra shape NAME:M:N:K:AT:BT:BATCH (repeatable)")
     args = ap.parse_args()
     lib = _lib.load()
     torch.cuda.init()
@@ -64,7 +66,11 @@ def main():
     cfg = baseline_config(args.config)
     variants = [(int(v), int(d)) for v in args.variants.split(",") for d in args.diag.split(",")]
     want = set(args.shapes.split(",")) if args.shapes else None
-    sh = [s for s in shapes(cfg) if want is None or s[0] in want]
+    extra = []
+    for e in args.extra:
+        f = e.split(":")
+        extra.append((f[0], *[int(v) for v in f[1:7]], 0))
+    sh = [s for s in shapes(cfg) if want is None or s[0] in want] + extra
     res = {}
     for _ in range(args.rounds):
         for name, M, N, K, at, bt, batch, epi in sh:
