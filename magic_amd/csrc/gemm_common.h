@@ -432,6 +432,8 @@ __device__ __forceinline__ void epilogue_rm_w(const Params& p, const Tile& t, WB
   float sf[LD ? NQ : 1][8];
   uint4 sb[LD ? NQ : 1], sbn[LD ? NQ : 1];
   if (bsrc) load_band(0, true, sf, sb);
+  // every target pixel of the batch 0 or 1 (the de-interleave's flag): no per-pixel test
+  const bool allbin = EPI == EPI_BCEB && e.xnb && *e.xnb == 0;
   // One band per iteration of a NON-unrolled loop: the band's accumulators are always acc[0]
   // (the blocks rotate down after the writer), so the epilogue code is emitted once instead of
   // MI times (37.6 -> 13.6 KB for the 256x256 ACT kernel; no time change measured).
@@ -485,15 +487,24 @@ __device__ __forceinline__ void epilogue_rm_w(const Params& p, const Tile& t, WB
             // other term is exactly 0 -- at one logarithm per pixel instead of two
             // (hardware log2 scaled by ln 2: v_log_f32 + one multiply, where __logf expands to
             // ~12 instructions of denormal scaling and extended-precision correction)
-            bool bin = true;
+            bool bin = allbin;
+            if (!bin) {
+              bool b = true;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) bin &= (sv[j] == 0.f) | (sv[j] == 1.f);
-            if (__all(bin)) {
+              for (int j = 0; j < 8; ++j) b &= (sv[j] == 0.f) | (sv[j] == 1.f);
+              bin = __all(b);
+            }
+            if (bin) {
+              float bt[8];
 #pragma unroll
-              for (int j = 0; j < 8; ++j) {
-                const float bt = __builtin_amdgcn_logf(sv[j] != 0.f ? yv[j] : 1.f - yv[j]) *
-                                 0.693147180559945309f;
-                rs += j < nv ? bt : 0.f;
+              for (int j = 0; j < 8; ++j)
+                bt[j] = __builtin_amdgcn_logf(sv[j] != 0.f ? yv[j] : 1.f - yv[j]) * 0.693147180559945309f;
+              if (nv == 8) {  // (the same sum in the same order, without the column mask)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) rs += bt[j];
+              } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) rs += j < nv ? bt[j] : 0.f;
               }
             } else {
 #pragma unroll

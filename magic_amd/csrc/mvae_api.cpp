@@ -727,6 +727,7 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
       const Planes xp = planes_of(c, c->xs);
       c->f_out.epi.xp = xp.p + (size_t)B * c->ldx;
       c->f_out.epi.xdyn = c->dyn;
+      c->f_out.epi.xnb = c->dyn + 2;
     } else {
       c->x32mask |= 2;  // the native fp32 BCE GEMM reads the fp32 target rows
     }
@@ -1040,6 +1041,7 @@ static int run(mvae_ctx* ctx, const GemmDesc& d, hipStream_t st, int r = -1) {
     GemmDesc dd = d;
     if (dd.dynA == ctx->dyn) dd.dynA = ctx->dyn_cur;
     if (dd.epi.xdyn == ctx->dyn) dd.epi.xdyn = ctx->dyn_cur;
+    if (dd.epi.xnb == ctx->dyn + 2) dd.epi.xnb = ctx->dyn_cur + 2;
     MV_CHECK(gemm_run(dd, ws, ctx->ws_elems, st));
     return MVAE_OK;
   }
@@ -1734,6 +1736,7 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
           if (e == hipSuccess) e = hipMemsetAsync(reinterpret_cast<char*>(xpl) + (size_t)M * ldc * 2, 0, 16, st);
           d.epi.xp = xpl;
           d.epi.xdyn = reinterpret_cast<const int*>(reinterpret_cast<char*>(xpl) + (size_t)M * ldc * 2);
+          d.epi.xnb = d.epi.xdyn + 2;  // (the zeroed 16 B: binarized targets)
         }
       }
     }

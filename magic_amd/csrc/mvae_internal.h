@@ -43,6 +43,9 @@ struct GemmEpi {
   // pixel of the batch is exact in bf16; the fp32 rows are then never written.
   const unsigned short* xp = nullptr;
   const int* xdyn = nullptr;
+  // BCE: *xnb == 0 when every target pixel is 0 or 1 (the de-interleave's second flag word, two
+  // slots past xdyn's): the epilogue then takes the one-logarithm form without testing pixels
+  const int* xnb = nullptr;
   float scale = 1.f;            // BCE: 1/global_batch
   float* y = nullptr;           // BCE: optional sigmoid output
   int ldy = 0;

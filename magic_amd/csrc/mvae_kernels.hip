@@ -56,8 +56,12 @@ __device__ __forceinline__ uint2 pack4(unsigned short a, unsigned short b, unsig
 __global__ void deinterleave_vec_kernel(const float4* __restrict__ x, float* __restrict__ xs,
                                         unsigned short* __restrict__ xp, int* __restrict__ dyn,
                                         int B, int D, int ldx, int f32mask, int* __restrict__ dyn_next) {
-  // the other slot of the flag, for the next de-interleave (no per-step memset launch)
-  if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) *dyn_next = 0;
+  // the other slot of the flags, for the next de-interleave (no per-step memset launch); this
+  // form does not test for 0/1 pixels: it raises the not-binary word (dyn[2]) unconditionally
+  if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) {
+    if (dyn_next) dyn_next[0] = dyn_next[2] = 0;
+    if (dyn) atomicOr(dyn + 2, 1);
+  }
   const int b = blockIdx.y;
   const int q = blockIdx.x * blockDim.x + threadIdx.x;  // pixel quad
   bool nz = false;
@@ -135,20 +139,33 @@ template <int NQ>
 __global__ void deinterleave_vecn_kernel(const float4* __restrict__ x, float* __restrict__ xs,
                                          unsigned short* __restrict__ xp, int* __restrict__ dyn,
                                          int B, int D, int ldx, int f32mask, int* __restrict__ dyn_next) {
-  // the other slot of the flag, for the next de-interleave (no per-step memset launch)
-  if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) *dyn_next = 0;
+  // the other slot of the flags, for the next de-interleave (no per-step memset launch)
+  if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) dyn_next[0] = dyn_next[2] = 0;
   constexpr int NP = 4 * NQ;  // pixels per thread
   const int b = blockIdx.y;
   const int q = blockIdx.x * blockDim.x + threadIdx.x;
-  bool nz = false;
+  bool nz = false, nb = false;
   if (q * NP < D) {
     const float4* src = x + ((size_t)b * 3 * D) / 4 + 3 * NQ * q;
     float4 v[3 * NQ];
 #pragma unroll
     for (int i = 0; i < 3 * NQ; ++i) v[i] = src[i];
+    // some value of the three channels neither 0 nor 1 (the BCE target is one of them)
+#pragma unroll
+    for (int i = 0; i < 3 * NQ; ++i) {
+      const float e[4] = {v[i].x, v[i].y, v[i].z, v[i].w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) nb |= (e[j] != 0.f) & (e[j] != 1.f);
+    }
     nz = deint_put<NQ>(v, xs, xp, B, b, (size_t)NP * q, ldx, f32mask);
   }
-  if (dyn && __ballot(nz) != 0 && (threadIdx.x & 63) == 0) atomicOr(dyn, 1);
+  if (dyn) {  // (the ballots with every lane of the wave active)
+    const bool anz = __ballot(nz) != 0, anb = __ballot(nb) != 0;
+    if ((threadIdx.x & 63) == 0) {
+      if (anz) atomicOr(dyn, 1);
+      if (anb) atomicOr(dyn + 2, 1);
+    }
+  }
 }
 
 // (diagnostics) persistent form: gridDim.x workgroups stride over the B x D/8 pixel groups
@@ -169,8 +186,11 @@ __global__ void deinterleave_persist_kernel(const float4* __restrict__ x, unsign
 __global__ void deinterleave_scalar_kernel(const float* __restrict__ x, float* __restrict__ xs,
                                            unsigned short* __restrict__ xp, int* __restrict__ dyn,
                                            int B, int D, int ldx, int f32mask, int* __restrict__ dyn_next) {
-  // the other slot of the flag, for the next de-interleave (no per-step memset launch)
-  if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) *dyn_next = 0;
+  // the other slot of the flags (see deinterleave_vec_kernel: no 0/1 test here)
+  if ((blockIdx.x | blockIdx.y | threadIdx.x) == 0) {
+    if (dyn_next) dyn_next[0] = dyn_next[2] = 0;
+    if (dyn) atomicOr(dyn + 2, 1);
+  }
   const int b = blockIdx.y;
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   bool nz = false;
