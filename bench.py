@@ -118,6 +118,8 @@ def region_flops(cfg, name: str) -> float:
             return 3 * B * conv2
         if name in ("conv2_dgrad", "conv2_wgrad"):
             return 4 * B * conv2
+    if name == "enc_fwd_chain":  # the hidden layers 1 .. n-1 in one launch
+        return sum(2.0 * 3 * B * widths[i] * widths[i + 1] for i in range(1, len(cfg.enc)))
     if name.startswith("enc_fwd_"):
         i = int(name.rsplit("_", 1)[1])
         return 2.0 * 3 * B * widths[i] * widths[i + 1]

@@ -117,6 +117,10 @@ struct mvae_ctx {
   int x32dyn = 0;        // ... written only when *dyn != 0 (the BCE target, else read as bf16)
   // schedule (each GEMM tagged with its timing region)
   std::vector<GemmDesc> fwd_enc;  // encoder layers + head
+  // the hidden layers fwd_enc[1 .. nenc-1] as one launch (enc_chain.hip; create option enc_chain)
+  bool chain = false;
+  ChainArgs chain_args;
+  int chain_r = 0;
   GemmDesc f_d1, f_d2, f_out;
   GemmDesc f_out_a, f_out_b;  // f_out as whole rounds of 256x256 tiles + the rest (f_split)
   bool f_split = false;
@@ -418,6 +422,9 @@ struct CreateOpts {
   int diag_skip_deint = 0;  // diagnostics: de-interleave only the first batch (the step's time
                             // without its streaming pass; results meaningless)
   int diag_shadow_deint = 0, diag_shadow_at = 0;  // diagnostics: see mvae_ctx::diag_shadow
+  int enc_chain = 1;    // bf16 mode: the encoder's hidden layers in one launch (0: one GEMM each)
+  int enc_chain_rows = 0;  // ... its rows per workgroup forced (16..96, multiple of 16; 0 auto)
+  int diag_chain = 0;      // ... its timing ablations (ChainArgs::diag; results meaningless)
   int conv2_nw = 8, conv2_tpb = 1, conv2_fpw = 2, conv2_wg = 8, conv2_half = 1, conv2_nchunk = 0;
 };
 
@@ -447,6 +454,9 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "diag_skip_deint" && in(0, 1)) o->diag_skip_deint = (int)v;
     else if (k == "diag_shadow_deint" && in(-1, 1 << 16)) o->diag_shadow_deint = (int)v;
     else if (k == "diag_shadow_at" && in(0, 2)) o->diag_shadow_at = (int)v;
+    else if (k == "enc_chain" && in(0, 1)) o->enc_chain = (int)v;
+    else if (k == "diag_chain" && in(0, 7)) o->diag_chain = (int)v;
+    else if (k == "enc_chain_rows" && (v == 0 || (in(16, 96) && v % 16 == 0))) o->enc_chain_rows = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
     else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
     else if (k == "conv2_fpw" && (v == 2 || v == 4)) o->conv2_fpw = (int)v;
@@ -837,6 +847,30 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
   wsz(c->f_out);
   if (c->conv) wsz(c->bwd_feat);
   c->ws_elems = ws;
+  // the hidden encoder layers as one launch: bf16 planes in and out, tanh / elu epilogues writing
+  // planes only, widths that fit the kernel's 512-column activation block
+  if (opt.enc_chain && c->np == 1 && c->nenc >= 3 && c->nenc - 1 <= 4) {
+    bool ok = true;
+    ChainArgs& ca = c->chain_args;
+    ca.x = c->fwd_enc[1].Ap;
+    ca.ldx = c->fwd_enc[1].lda;
+    ca.M = c->fwd_enc[1].M;
+    ca.nl = c->nenc - 1;
+    ca.act = c->fwd_enc[1].epi.act;
+    ca.rows = opt.enc_chain_rows;
+    ca.diag = opt.diag_chain;
+    for (int i = 1; i < c->nenc; ++i) {
+      const GemmDesc& d = c->fwd_enc[i];
+      ok = ok && d.prec == GEMM_BF16 && !d.valu && d.epi.mode == EPI_ACT && d.epi.c32 == 0 &&
+           d.epi.cp && d.epi.ncp == 1 && d.epi.padw == 2 && d.Ap && d.Bp && d.batch == 1 && !d.at &&
+           !d.bt && d.K <= 512 && d.N <= 511 && d.M == ca.M && d.epi.act == ca.act;
+      ChainLayer& cl = ca.l[i - 1];
+      cl.w = d.Bp; cl.ldw = d.ldb; cl.K = d.K; cl.N = d.N; cl.out = d.epi.cp; cl.ldo = d.ldc;
+      if (i > 1) ok = ok && d.Ap == c->fwd_enc[i - 1].epi.cp && d.lda == c->fwd_enc[i - 1].ldc;
+    }
+    c->chain = ok;
+    c->chain_r = region(c, "enc_fwd_chain");
+  }
   if (opt.plan_log) {
     // the GEMM plans of this context (diagnostics): shape, arithmetic, kernel, split-K + combine
     auto show = [&](const GemmDesc& d, int r) {
@@ -847,6 +881,9 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
                    (int)wide, wide ? gemm_bf16_wide_tm(d, ws) : 0, wide ? gemm_bf16_wide_tn(d, ws) : 0, sp);
     };
     for (size_t i = 0; i < c->fwd_enc.size(); ++i) show(c->fwd_enc[i], c->fwd_enc_r[i]);
+    if (c->chain)
+      std::fprintf(stderr, "[mvae plan] enc_fwd_chain    layers 1..%d in one launch, %d rows per workgroup\n",
+                   c->nenc - 1, enc_chain_rows(c->chain_args.M, c->chain_args.rows));
     show(c->f_d1, c->f_d1_r); show(c->f_d2, c->f_d2_r); show(c->f_out, c->f_out_r);
     for (size_t i = 0; i < c->bwd_dec.size(); ++i) show(c->bwd_dec[i], c->bwd_dec_r[i]);
     for (size_t i = 0; i < c->bwd_enc.size(); ++i) show(c->bwd_enc[i], c->bwd_enc_r[i]);
@@ -1125,6 +1162,12 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
     }
   }
   for (size_t i = 0; i < c->fwd_enc.size(); ++i) {
+    if (c->chain && i == 1) {  // the hidden layers 1 .. nenc-1
+      TimeScope ts(c, c->chain_r, st);
+      MV_CHECK(launch_enc_chain(c->chain_args, st));
+      i = c->nenc - 1;
+      continue;
+    }
     int rc = run(c, c->fwd_enc[i], st, c->fwd_enc_r[i]);
     if (rc) return rc;
   }

@@ -114,6 +114,28 @@ void gemm_bf16_wide_plan(const GemmDesc& d, size_t max_ws, int* split, int* tn, 
 // Number of column blocks the BCE epilogue writes per row (rowpart's inner dim).
 int gemm_bce_nblk(int N);
 
+// ---- the encoder's hidden layers in one launch (enc_chain.hip, bf16 planes) ----
+// layer: out = act(in W) on bf16 planes; W [K][ldw] (K incl. the bias row), N output columns,
+// out [M][ldo] with the row padding of GemmEpi::padw = 2 (1.0 at column N, zeros to round8(N+1))
+struct ChainLayer {
+  const unsigned short* w = nullptr;
+  int ldw = 0, K = 0, N = 0;
+  unsigned short* out = nullptr;
+  int ldo = 0;
+};
+struct ChainArgs {
+  const unsigned short* x = nullptr;  // the first layer's input plane [M][ldx] (padded rows)
+  int ldx = 0, M = 0, nl = 0, act = 0;
+  int rows = 0;  // rows per workgroup forced (create option enc_chain_rows; 0: enc_chain_rows)
+  int diag = 0;  // timing ablations (results meaningless): 1 no weight DMA after the first steps,
+                 // 2 no MFMAs, 4 no block copy-out (create option diag_chain)
+  ChainLayer l[4];
+};
+// rows per workgroup for M rows (a multiple of 16, <= 96; forced: a valid forced value wins)
+int enc_chain_rows(int M, int forced = 0);
+// K <= 512, N <= 511, 16-B aligned planes and strides multiple of 8, else hipErrorInvalidValue
+hipError_t launch_enc_chain(const ChainArgs& a, hipStream_t st);
+
 // ---- elementwise / reduction kernels (mvae_kernels.hip) ----
 // bf16 plane image of an fp32 buffer (same layout): planes at p + t*stride, t < n
 struct Planes {
