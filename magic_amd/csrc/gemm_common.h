@@ -396,6 +396,10 @@ __device__ __forceinline__ void epilogue_rm_w(const Params& p, const Tile& t, WB
   auto pass_full = [&](int nv) { return vec && (nv == 8 || (e.padw && nv > 0)); };
   constexpr bool bsrc = EPI == EPI_DACTB || EPI == EPI_BCEB;  // the operand is bf16
   // the operand rows of band mi's NQ passes: bf16 packed into sb (b16) or fp32 into sf
+  // every target pixel of the batch 0 or 1 (the de-interleave's flag): no per-pixel test, and
+  // the targets read as one bit per pixel when the de-interleave wrote them so (e.xbits)
+  const bool allbin = EPI == EPI_BCEB && e.xnb && *e.xnb == 0;
+  const bool tbits = allbin && e.xbits != nullptr;
   auto load_band = [&](int mi, bool b16, float (&sf)[LD ? NQ : 1][8], uint4 (&sb)[LD ? NQ : 1]) {
     if constexpr (LD) {
 #pragma unroll
@@ -405,7 +409,9 @@ __device__ __forceinline__ void epilogue_rm_w(const Params& p, const Tile& t, WB
         int sr = row < p.M ? row : p.M - 1;
         if constexpr (is_dact<EPI>) sr = sr >= e.remap_split ? sr - e.remap_shift : sr;
         const int ld_src = is_dact<EPI> ? e.ld_aux : e.ldx;
-        if (b16) {
+        if (EPI == EPI_BCEB && tbits) {  // byte col0 / 8 of the row: bit j = column col0 + j
+          sb[q] = make_uint4(nv > 0 ? (unsigned)e.xbits[(size_t)sr * e.ldbits + (col0 >> 3)] : 0u, 0u, 0u, 0u);
+        } else if (b16) {
           const unsigned short* src = (is_dact<EPI> ? e.auxp : e.xp) + (size_t)sr * ld_src + col0;
           if (pass_full(nv)) {
             sb[q] = *reinterpret_cast<const uint4*>(src);
@@ -432,8 +438,6 @@ __device__ __forceinline__ void epilogue_rm_w(const Params& p, const Tile& t, WB
   float sf[LD ? NQ : 1][8];
   uint4 sb[LD ? NQ : 1], sbn[LD ? NQ : 1];
   if (bsrc) load_band(0, true, sf, sb);
-  // every target pixel of the batch 0 or 1 (the de-interleave's flag): no per-pixel test
-  const bool allbin = EPI == EPI_BCEB && e.xnb && *e.xnb == 0;
   // One band per iteration of a NON-unrolled loop: the band's accumulators are always acc[0]
   // (the blocks rotate down after the writer), so the epilogue code is emitted once instead of
   // MI times (37.6 -> 13.6 KB for the 256x256 ACT kernel; no time change measured).
@@ -462,7 +466,10 @@ __device__ __forceinline__ void epilogue_rm_w(const Params& p, const Tile& t, WB
       if (nv > 0) {
         float sv[8];
         if constexpr (LD) {
-          if (bsrc) {
+          if (EPI == EPI_BCEB && tbits) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) sv[j] = (sb[q].x >> j) & 1u ? 1.f : 0.f;
+          } else if (bsrc) {
             const unsigned ww[4] = {sb[q].x, sb[q].y, sb[q].z, sb[q].w};
 #pragma unroll
             for (int j = 0; j < 4; ++j) {

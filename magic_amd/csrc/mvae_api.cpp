@@ -115,6 +115,8 @@ struct mvae_ctx {
   int* dyn_cur = nullptr;  // ... its slot of the last de-interleave (two slots, used in turn)
   int x32mask = 7;       // fp32 row blocks of xs the step reads (bit c: 0 rot, 1 lock, 2 key)
   int x32dyn = 0;        // ... written only when *dyn != 0 (the BCE target, else read as bf16)
+  unsigned char* xbits = nullptr;  // the BCE target (lock block) as bits (GemmEpi::xbits)
+  int ldbits = 0;
   // schedule (each GEMM tagged with its timing region)
   std::vector<GemmDesc> fwd_enc;  // encoder layers + head
   // the hidden layers fwd_enc[1 .. nenc-1] as one launch (enc_chain.hip; create option enc_chain)
@@ -738,6 +740,14 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
       c->f_out.epi.xp = xp.p + (size_t)B * c->ldx;
       c->f_out.epi.xdyn = c->dyn;
       c->f_out.epi.xnb = c->dyn + 2;
+      if (c->D % 8 == 0) {  // the 8-pixel de-interleave writes the target's bits beside its plane
+        c->ldbits = (c->D / 8 + 15) & ~15;
+        float* xb = nullptr;
+        ALLOC(xb, ((size_t)B * c->ldbits + 3) / 4);
+        c->xbits = reinterpret_cast<unsigned char*>(xb);
+        c->f_out.epi.xbits = c->xbits;
+        c->f_out.epi.ldbits = c->ldbits;
+      }
     } else {
       c->x32mask |= 2;  // the native fp32 BCE GEMM reads the fp32 target rows
     }
@@ -827,6 +837,7 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
       if (b.epi.cp) b.epi.cp = f.epi.cp + c0;
       if (b.epi.x) b.epi.x = f.epi.x + c0;
       if (b.epi.xp) b.epi.xp = f.epi.xp + c0;
+      if (b.epi.xbits) b.epi.xbits = f.epi.xbits + c0 / 8;  // (c0: a multiple of 256)
       b.epi.rp_ld = gemm_bce_nblk(f.N);
       b.epi.rp_off = c0 / 128;
       b.variant = 11;  // the ring kernel at 256x128 tiles
@@ -1117,7 +1128,7 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
     int* prev = c->dyn_cur ? c->dyn_cur : c->dyn;
     int* cur = c->dyn ? (prev == c->dyn ? c->dyn + 1 : c->dyn) : nullptr;
     MV_CHECK(launch_deinterleave(x, c->xs, planes_of(c, c->xs), cur, c->dyn ? prev : nullptr, c->B,
-                                 c->D, c->ldx, c->x32mask, c->x32dyn, st));
+                                 c->D, c->ldx, c->x32mask, c->x32dyn, st, c->xbits, c->ldbits));
     c->dyn_cur = cur;
   }
   if (c->diag_shadow && c->diag_shadow_at == 0 && draw == ENC_TRAIN) {

@@ -46,6 +46,10 @@ struct GemmEpi {
   // BCE: *xnb == 0 when every target pixel is 0 or 1 (the de-interleave's second flag word, two
   // slots past xdyn's): the epilogue then takes the one-logarithm form without testing pixels
   const int* xnb = nullptr;
+  // BCE: the target as one bit per pixel (byte c of row r: columns 8c .. 8c + 7, bit j = column
+  // 8c + j nonzero), valid while *xnb == 0: read instead of the bf16 plane, 16x fewer bytes
+  const unsigned char* xbits = nullptr;
+  int ldbits = 0;
   float scale = 1.f;            // BCE: 1/global_batch
   float* y = nullptr;           // BCE: optional sigmoid output
   int ldy = 0;
@@ -148,8 +152,11 @@ struct Planes {
 // planes 1-2 (3-plane mode) and the fp32 rows of the blocks in f32dyn_mask written. The flag has
 // two slots used in turn: each launch zeroes the other one (dyn_next, the next launch's dyn),
 // whose last readers ran before it on the stream.
+// xbits (optional): the lock block's pixels as bits (GemmEpi::xbits, ldbits bytes per row), written
+// by the 8-pixel form only (D % 8 == 0; the other forms raise the not-binary word instead)
 hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int* dyn_next,
-                               int B, int D, int ldx, int f32mask, int f32dyn_mask, hipStream_t st);
+                               int B, int D, int ldx, int f32mask, int f32dyn_mask, hipStream_t st,
+                               unsigned char* xbits = nullptr, int ldbits = 0);
 // (diagnostics) the bf16 plane-0 pass alone into xp: grid -1 the normal launch, > 0 that many
 // persistent 256-thread workgroups striding over the rows' 8-pixel groups
 hipError_t launch_deinterleave_grid(const float* x, unsigned short* xp, int B, int D, int ldx, int grid,

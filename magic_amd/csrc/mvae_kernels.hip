@@ -138,7 +138,8 @@ __device__ __forceinline__ bool deint_put(const float4* v, float* __restrict__ x
 template <int NQ>
 __global__ void deinterleave_vecn_kernel(const float4* __restrict__ x, float* __restrict__ xs,
                                          unsigned short* __restrict__ xp, int* __restrict__ dyn,
-                                         int B, int D, int ldx, int f32mask, int* __restrict__ dyn_next) {
+                                         int B, int D, int ldx, int f32mask, int* __restrict__ dyn_next,
+                                         unsigned char* __restrict__ xbits, int ldbits) {
   // the other slot of the flags, for the next de-interleave (no per-step memset launch)
   if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) dyn_next[0] = dyn_next[2] = 0;
   constexpr int NP = 4 * NQ;  // pixels per thread
@@ -158,6 +159,16 @@ __global__ void deinterleave_vecn_kernel(const float4* __restrict__ x, float* __
       for (int j = 0; j < 4; ++j) nb |= (e[j] != 0.f) & (e[j] != 1.f);
     }
     nz = deint_put<NQ>(v, xs, xp, B, b, (size_t)NP * q, ldx, f32mask);
+    if (xbits) {  // the lock channel (element 3 j of pixel j) as bits, 8 pixels per byte
+      static_assert(NQ == 2, "one byte per thread");
+      const float e[24] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                           v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w,
+                           v[4].x, v[4].y, v[4].z, v[4].w, v[5].x, v[5].y, v[5].z, v[5].w};
+      unsigned byte = 0;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) byte |= (e[3 * j] != 0.f ? 1u : 0u) << j;
+      xbits[(size_t)b * ldbits + q] = (unsigned char)byte;
+    }
   }
   if (dyn) {  // (the ballots with every lane of the wave active)
     const bool anz = __ballot(nz) != 0, anb = __ballot(nb) != 0;
@@ -826,14 +837,16 @@ __global__ void mvae_region_marker() {}
 }  // namespace
 
 hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int* dyn_next,
-                               int B, int D, int ldx, int f32mask, int f32dyn_mask, hipStream_t st) {
+                               int B, int D, int ldx, int f32mask, int f32dyn_mask, hipStream_t st,
+                               unsigned char* xbits, int ldbits) {
   // 8 pixels per thread (4 and 16 measured slower, profiles/r4/r4y_deinterleave.txt; an LDS-staged
   // form with lane-contiguous loads too, r4an_deinterleave_lds_rejected.txt); 4 when D % 8 != 0
   const bool al = (reinterpret_cast<uintptr_t>(x) % 16) == 0;
   if ((D % 8) == 0 && al && (ldx % 8) == 0) {
     dim3 g(nblocks(D / 8, 256), B);
     hipLaunchKernelGGL(deinterleave_vecn_kernel<2>, g, dim3(256), 0, st,
-                       reinterpret_cast<const float4*>(x), xs, xp.p, dyn, B, D, ldx, f32mask, dyn_next);
+                       reinterpret_cast<const float4*>(x), xs, xp.p, dyn, B, D, ldx, f32mask, dyn_next,
+                       xbits, ldbits);
   } else if ((D % 4) == 0 && (reinterpret_cast<uintptr_t>(x) % 16) == 0 && (ldx % 4) == 0) {
     dim3 g(nblocks(D / 4, 256), B);
     hipLaunchKernelGGL(deinterleave_vec_kernel, g, dim3(256), 0, st,
@@ -856,7 +869,7 @@ hipError_t launch_deinterleave_grid(const float* x, unsigned short* xp, int B, i
   if (grid < 0) {
     dim3 g(nblocks(D / 8, 256), B);
     hipLaunchKernelGGL(deinterleave_vecn_kernel<2>, g, dim3(256), 0, st, reinterpret_cast<const float4*>(x),
-                       nullptr, xp, nullptr, B, D, ldx, 0, nullptr);
+                       nullptr, xp, nullptr, B, D, ldx, 0, nullptr, nullptr, 0);
   } else if (grid > 0) {
     hipLaunchKernelGGL(deinterleave_persist_kernel, dim3(grid), dim3(256), 0, st,
                        reinterpret_cast<const float4*>(x), xp, B, D, ldx);
