@@ -254,20 +254,23 @@ struct E8 {
     const int pb = (pp.pab >> (4 * pr + 2)) & 3;
     lb.template issue<H>(Bm + pb * pp.pB, pp.g.ldb, t.ks + kt * EBK, t.ke, smem + (4 + 2 * H + Bf) * EH, wave);
   }
-  // k-tile `it` (its images in buffer Bf); (kt1, pr1), (kt2, pr2): (k-tile, pair) of it+1, it+2
+  // k-tile `it` (its images in buffer Bf); (kt1, pr1), (kt2, pr2): (k-tile, pair) of it+1, it+2;
+  // ka1: it+1's A image is the one its buffer holds (from it-1: not copied again), ka2 / kb2: it+2's
+  // A / B images likewise (from it)
   template <int Bf>
   __device__ __forceinline__ void tile(const PParams& pp, const Tile& t, int it, int total, int kt1, int pr1,
-                                       int kt2, int pr2) {
+                                       int kt2, int pr2, bool ka1, bool ka2, bool kb2) {
     constexpr int Bn = Bf ^ 1;
     // stamped builds' A/B switches (results meaningless): diag 1 = no DMA after the prologue,
     // 64 = no fragment reads
     const bool dma = !ST || !(pp.diag & 1), rdf = !ST || !(pp.diag & 64);
     const bool h1 = it + 1 < total && dma, h2 = it + 2 < total && dma;
+    const bool ia2 = h2 && !ka2, ib2 = h2 && !kb2;
     // p1 (0,0)
     if (rdf) rd_b<0, Bf>(fb0);
     __builtin_amdgcn_sched_barrier(0);
     if (rdf) rd_a<0, Bf>(fa0);
-    if (h1) issue_a<1, Bn>(pp, t, kt1, pr1);
+    if (h1 && !ka1) issue_a<1, Bn>(pp, t, kt1, pr1);
     // the B-sub 0 reads (issued first) retired: B0 is restaged in p2
     // (the A-sub 0 reads: 8 ds_read_b128, or 16 transposing reads -- the count saturates at 15)
     if constexpr (KA) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
@@ -277,23 +280,23 @@ struct E8 {
     sbar<1>();
     // p2 (0,1)
     if (rdf) rd_b<1, Bf>(fb1);
-    if (h2) issue_b<0, Bf>(pp, t, kt2, pr2);
+    if (ib2) issue_b<0, Bf>(pp, t, kt2, pr2);
     sbar<2>();
     mfma_q<0, 1>(fa0, fb1);
     sbar<3>();
     // p3 (1,1)
     if (rdf) rd_a<1, Bf>(fa1);
-    if (h2) issue_a<0, Bf>(pp, t, kt2, pr2);
+    if (ia2) issue_a<0, Bf>(pp, t, kt2, pr2);
     sbar<4>();
     mfma_q<1, 1>(fa1, fb1);
     sbar<5>();
-    // p4 (1,0)
-    if (h2) {
-      issue_b<1, Bf>(pp, t, kt2, pr2);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // k-tile it+1 landed
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // p4 (1,0): k-tile it+1 landed -- what stays in flight is the halves of it+2 issued in this
+    // tile (2 DMA instructions each)
+    if (ib2) issue_b<1, Bf>(pp, t, kt2, pr2);
+    if (ib2 && ia2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (ib2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (ia2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     sbar<6>();
     mfma_q<1, 0>(fa1, fb0);
     sbar<7>();
@@ -357,17 +360,36 @@ __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
   const bool lag = __builtin_amdgcn_readfirstlane(wave) >= 4 && !(ST && (pp.diag & 128));
 
   if (total > 0) {
-    // (k-tile, pair) cursors of tiles it+1 and it+2
-    int kt1 = 0, pr1 = 0, kt2 = 0, pr2 = 0;
-    auto adv = [&](int& kt, int& pr) { if (++pr == np) { pr = 0; ++kt; } };
+    // The (k-tile, pair) walk. Default: pairs innermost. reuse (f32x plane pairs): k-tiles in
+    // twos, pairs between -- (k0,p0) (k1,p0) (k0,p1) (k1,p1) ... -- so an iteration and the one
+    // two before it (the same LDS buffer) share the k-tile, and an operand plane they share is
+    // not copied again (binary pixels, 3 pairs: 2 of 6 A images copied; 6 pairs: 16 of 24
+    // images). Cursor = (group g of two k-tiles, index r within it).
+    struct Cur { int g, r, kt, pr; };
+    const bool rw = pp.reuse != 0;
+    auto set = [&](Cur& c) {
+      if (!rw) { c.kt = c.g; c.pr = c.r; return; }
+      if (2 * c.g + 1 < nkt) { c.kt = 2 * c.g + (c.r & 1); c.pr = c.r >> 1; }
+      else { c.kt = 2 * c.g; c.pr = c.r; }
+    };
+    auto adv = [&](Cur& c) {
+      const int span = !rw ? np : (2 * c.g + 1 < nkt ? 2 * np : np);
+      if (++c.r == span) { c.r = 0; ++c.g; }
+      set(c);
+    };
+    auto pa_of = [&](int pr) { return (pp.pab >> (4 * pr)) & 3; };
+    auto pb_of = [&](int pr) { return (pp.pab >> (4 * pr + 2)) & 3; };
+    // cursors of iterations it-1 .. it+2
+    Cur cm{0, 0, 0, 0}, c0{0, 0, 0, 0}, c1{0, 0, 0, 0}, c2{0, 0, 0, 0};
+    set(c0);
+    c1 = c0; adv(c1);
+    c2 = c1; adv(c2);
     // prologue: A0 B0 B1 A1 of k-tile 0, then B0 A0 B1 of k-tile 1 (its A1: tile 0's p1)
     s.template issue_a<0, 0>(pp, t, 0, 0);
     s.template issue_b<0, 0>(pp, t, 0, 0);
     s.template issue_b<1, 0>(pp, t, 0, 0);
     s.template issue_a<1, 0>(pp, t, 0, 0);
-    adv(kt1, pr1);
-    kt2 = kt1; pr2 = pr1;
-    adv(kt2, pr2);
+    int kt1 = c1.kt, pr1 = c1.pr, kt2 = c2.kt, pr2 = c2.pr;
     if (total > 1) {
       s.template issue_b<0, 1>(pp, t, kt1, pr1);
       s.template issue_a<0, 1>(pp, t, kt1, pr1);
@@ -385,12 +407,19 @@ __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
       st_r0 = __builtin_amdgcn_s_memrealtime();
       st_t0 = s.st_last = __builtin_amdgcn_s_memtime();
     }
+    // iteration j's image (A or B) is already in its buffer: iteration j-2 had the same k-tile
+    // and plane (it+1's A: from it-1 -- cm; it+2's: from it -- c0)
+    auto ka = [&](const Cur& a, const Cur& b, int j) { return rw && j >= 2 && a.kt == b.kt && pa_of(a.pr) == pa_of(b.pr); };
+    auto kb = [&](const Cur& a, const Cur& b, int j) { return rw && j >= 2 && a.kt == b.kt && pb_of(a.pr) == pb_of(b.pr); };
+    auto step = [&]() { cm = c0; c0 = c1; c1 = c2; adv(c2); };
     for (int it = 0; it < total; it += 2) {
-      s.template tile<0>(pp, t, it, total, kt1, pr1, kt2, pr2);
-      kt1 = kt2; pr1 = pr2; adv(kt2, pr2);
+      s.template tile<0>(pp, t, it, total, c1.kt, c1.pr, c2.kt, c2.pr, ka(c1, cm, it + 1), ka(c2, c0, it + 2),
+                         kb(c2, c0, it + 2));
+      step();
       if (it + 1 < total) {
-        s.template tile<1>(pp, t, it + 1, total, kt1, pr1, kt2, pr2);
-        kt1 = kt2; pr1 = pr2; adv(kt2, pr2);
+        s.template tile<1>(pp, t, it + 1, total, c1.kt, c1.pr, c2.kt, c2.pr, ka(c1, cm, it + 2),
+                           ka(c2, c0, it + 3), kb(c2, c0, it + 3));
+        step();
       }
     }
     if (!lag) bar();

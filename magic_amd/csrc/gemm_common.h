@@ -39,6 +39,9 @@ struct PParams {
   const int* dyn;                   // A residual planes nonzero? (nullptr: use all pairs)
   int diag;                         // timing diagnostics: bit 0 = no operand copies after the
                                     // prologue (the k-loop multiplies stale LDS images)
+  int reuse;                        // eight-phase kernel: (k-tile, pair) iterations in pairs of
+                                    // k-tiles, pairs between, and an operand image not copied
+                                    // again when its buffer already holds it (gemm_bf16e.hip)
   unsigned long long* stamps;       // stamped diagnostics builds (ST): 8 slots per workgroup
                                     // {start, prologue landed, k-loop done, end, stores issued}
 };
