@@ -1,13 +1,17 @@
 #!/bin/bash
 # The current GPU session (overwritten per session; earlier sessions are in git history):
 #   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r5w (r5v repeated, HEAD's library first in each pair, 100 steps): the eight-phase kernel's image-reusing walk for f32x plane pairs (k-tiles in twos, pairs
-# between; an operand image its buffer already holds is not copied again): tests, then whole
-# steps against HEAD's library (libmvae_head.so), alternating, C2 (f32x) / C3.
+# r5x: verification of the tree: full GPU suite, smoke, the default bench line (CPU baseline + PMC
+# traffic + configs block), per-config rocprofv3 kernel-trace runs (C2, C3, C5).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 100"
-r() { echo "r5w_$1|120|$3 python bench.py --config $2 $BQ > gpurun_out/r5w_$1.json"; }
-H="MVAE_LIB=magic_amd/libmvae_head.so"
+export TMPDIR=/tmp
+PT="python -u -m pytest -q --maxfail=10 --timeout 120 --timeout-method thread -p no:cacheprovider"
+RP="rocprofv3 --kernel-trace --stats -f csv"
+BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 10 --warmup 3"
 bash tools/gpu_steps.sh \
-  "$(r c2_h1 C2 "$H")" "$(r c2_n1 C2)" "$(r c2_h2 C2 "$H")" "$(r c2_n2 C2)" "$(r c2_h3 C2 "$H")" "$(r c2_n3 C2)" \
-  "$(r c2_h4 C2 "$H")" "$(r c2_n4 C2)" "$(r c3_h1 C3 "$H")" "$(r c3_n1 C3)" "$(r c3_h2 C3 "$H")" "$(r c3_n2 C3)"
+  "r5x_tests|400|$PT tests -m gpu" \
+  "r5x_smoke|120|python -c 'import __graft_entry__ as g; g.smoke()'" \
+  "r5x_bench|500|python bench.py > gpurun_out/r5x_bench.json 2> gpurun_out/r5x_bench.err" \
+  "r5x_prof_c2|150|$RP -d gpurun_out/r5x_prof_c2 -o c2 -- python bench.py --config C2 $BQ" \
+  "r5x_prof_c3|150|$RP -d gpurun_out/r5x_prof_c3 -o c3 -- python bench.py --config C3 $BQ" \
+  "r5x_prof_c5|150|$RP -d gpurun_out/r5x_prof_c5 -o c5 -- python bench.py --config C5 $BQ"
