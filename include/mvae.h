@@ -185,7 +185,8 @@ int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* cou
  * chunks that finish -- and can be all-reduced -- one after another; "early_adam" (default 0)
  * lets mvae_adam update the blocks after the layer-0 block on the side stream as soon as the
  * backward has written their gradients (beside the layer-0 weight gradient): only for callers
- * that do not modify MVAE_BUF_GRADS between mvae_backward and mvae_adam (no all-reduce);
+ * that neither read nor modify MVAE_BUF_GRADS between mvae_backward and mvae_adam (no
+ * all-reduce): the caller's stream then joins the side stream in mvae_adam;
  * mvae_train_step uses it in the bf16 and f32x modes; "bce_split" (default 1) runs a BCE head whose
  * 256x256 tiles leave a partial last round as the whole rounds plus 256x128 tiles for the rest
  * (the same results). */
