@@ -217,7 +217,8 @@ static hipEvent_t take_event(mvae_ctx* c) {
     return e;
   }
   hipEvent_t e = nullptr;
-  (void)hipEventCreate(&e);
+  // timing only: no system-scope fence (a cache writeback + invalidate per record otherwise)
+  (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
   return e;
 }
 
@@ -914,7 +915,8 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
     }
     for (int i = 0; se == hipSuccess && i < 16; ++i) {
       hipEvent_t ev = nullptr;
-      se = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+      // stream-to-stream ordering on this device only: no system-scope fence
+      se = hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventDisableSystemFence);
       if (se == hipSuccess) c->sync_ev.push_back(ev);
     }
     if (se != hipSuccess) {
