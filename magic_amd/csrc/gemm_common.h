@@ -117,13 +117,19 @@ __device__ __forceinline__ int xcd_remap(int b, int nwg) {
 __device__ __forceinline__ float bf16_bits_to_f32(unsigned short b) {
   return __uint_as_float((unsigned)b << 16);
 }
-// BCE epilogues: EPI_BCE reads the fp32 target, EPI_BCEB its bf16 plane (exact while *xdyn == 0,
-// i.e. every pixel of the batch is a bf16 value). With xdyn set both are launched and the one
-// that does not match *xdyn returns at once (uniform branch at kernel entry).
+// BCE epilogues: EPI_BCE reads the fp32 target; EPI_BCEB reads its bf16 plane while *xdyn == 0
+// (every pixel of the batch a bf16 value) and the fp32 target otherwise -- one launch, the
+// choice a uniform branch in the epilogue (bce_x16). An EPI_BCE launch given xdyn returns at once
+// when the plane applies (the two-launch form; gemm_run launches EPI_BCEB alone).
 template <int EPI>
 __device__ __forceinline__ bool epi_skip(const GemmEpi& e) {
-  if constexpr (EPI == EPI_BCE || EPI == EPI_BCEB)
-    return e.xdyn != nullptr && ((*e.xdyn == 0) != (EPI == EPI_BCEB));
+  if constexpr (EPI == EPI_BCE) return e.xdyn != nullptr && *e.xdyn == 0;
+  return false;
+}
+// the BCE target read from its bf16 plane?
+template <int EPI>
+__device__ __forceinline__ bool bce_x16(const GemmEpi& e) {
+  if constexpr (EPI == EPI_BCEB) return e.xdyn == nullptr || *e.xdyn == 0;
   return false;
 }
 // -log-likelihood term of one pixel, TF semantics log(y^x (1-y)^(1-x)) with pow(0,0) = 1 and
@@ -208,6 +214,7 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
   // the stores may alias the loads.)
   constexpr bool BCE = EPI == EPI_BCE || EPI == EPI_BCEB;
   constexpr bool READS = is_dact<EPI> || BCE;
+  const bool x16 = bce_x16<EPI>(e);
   const float* __restrict__ src = is_dact<EPI> ? e.aux : e.x;
   const int lds_ = is_dact<EPI> ? e.ld_aux : e.ldx;
   // not unrolled: the block's accumulators are acc[0], rotated down after each block (one copy
@@ -225,7 +232,7 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
         for (int ni = 0; ni < NI; ++ni) {
           int col = cbase + ni * 32;
           col = col < p.N ? col : p.N - 1;
-          if constexpr (EPI == EPI_BCEB) sv[r][ni] = bf16_bits_to_f32(e.xp[(size_t)sr * lds_ + col]);
+          if (EPI == EPI_BCEB && x16) sv[r][ni] = bf16_bits_to_f32(e.xp[(size_t)sr * lds_ + col]);
           else if constexpr (is_dact<EPI>)
             sv[r][ni] = e.auxp ? bf16_bits_to_f32(e.auxp[(size_t)sr * lds_ + col]) : src[(size_t)sr * lds_ + col];
           else sv[r][ni] = src[(size_t)sr * lds_ + col];
@@ -397,13 +404,14 @@ __device__ __forceinline__ void epilogue_rm_w(const Params& p, const Tile& t, WB
   };
   // whole-chunk access of a partial last chunk (GemmEpi::padw)
   auto pass_full = [&](int nv) { return vec && (nv == 8 || (e.padw && nv > 0)); };
-  constexpr bool bsrc = EPI == EPI_DACTB || EPI == EPI_BCEB;  // the operand is bf16
+  const bool bsrc = EPI == EPI_DACTB || bce_x16<EPI>(e);  // the operand is bf16
   // the operand rows of band mi's NQ passes: bf16 packed into sb (b16) or fp32 into sf
   // every target pixel of the batch 0 or 1 (the de-interleave's flag): no per-pixel test, and
   // the targets read as one bit per pixel when the de-interleave wrote them so (e.xbits)
   const bool allbin = EPI == EPI_BCEB && e.xnb && *e.xnb == 0;
   const bool tbits = allbin && e.xbits != nullptr;
-  auto load_band = [&](int mi, bool b16, float (&sf)[LD ? NQ : 1][8], uint4 (&sb)[LD ? NQ : 1]) {
+  constexpr int SFN_ = (LD && EPI != EPI_BCEB) ? NQ : 1;
+  auto load_band = [&](int mi, bool b16, float (&sf)[SFN_][8], uint4 (&sb)[LD ? NQ : 1]) {
     if constexpr (LD) {
 #pragma unroll
       for (int q = 0; q < NQ; ++q) {
@@ -425,7 +433,7 @@ __device__ __forceinline__ void epilogue_rm_w(const Params& p, const Tile& t, WB
             sb[q] = make_uint4((unsigned)h[0] | (unsigned)h[1] << 16, (unsigned)h[2] | (unsigned)h[3] << 16,
                                (unsigned)h[4] | (unsigned)h[5] << 16, (unsigned)h[6] | (unsigned)h[7] << 16);
           }
-        } else {
+        } else if constexpr (EPI != EPI_BCEB) {
           const float* src = (is_dact<EPI> ? e.aux : e.x) + (size_t)sr * ld_src + col0;
           if (pass_full(nv)) ld8f(src, sf[q]);
           else
@@ -438,7 +446,10 @@ __device__ __forceinline__ void epilogue_rm_w(const Params& p, const Tile& t, WB
   // bf16 operands are loaded one band ahead (issued before band mi-1's transpose and passes),
   // so their latency hides behind a whole band of work; fp32 operands (twice the registers:
   // double-buffered they spill) at the start of their own band, before its LDS transpose
-  float sf[LD ? NQ : 1][8];
+  // (the combined BCE epilogue reads its rare fp32 target per pass instead: beside the bf16
+  // double buffer a band of fp32 operands spilled)
+  constexpr int SFN = (LD && EPI != EPI_BCEB) ? NQ : 1;
+  float sf[SFN][8];
   uint4 sb[LD ? NQ : 1], sbn[LD ? NQ : 1];
   if (bsrc) load_band(0, true, sf, sb);
   // One band per iteration of a NON-unrolled loop: the band's accumulators are always acc[0]
@@ -479,6 +490,12 @@ __device__ __forceinline__ void epilogue_rm_w(const Params& p, const Tile& t, WB
               sv[2 * j] = __uint_as_float(ww[j] << 16);
               sv[2 * j + 1] = __uint_as_float(ww[j] & 0xffff0000u);
             }
+          } else if constexpr (EPI == EPI_BCEB) {  // the fp32 target, read here (see sf)
+            const float* src = e.x + (size_t)(row < p.M ? row : p.M - 1) * e.ldx + col0;
+            if (full) ld8f(src, sv);
+            else
+#pragma unroll
+              for (int j = 0; j < 8; ++j) sv[j] = j < nv ? src[j] : 0.f;
           } else {
 #pragma unroll
             for (int j = 0; j < 8; ++j) sv[j] = sf[q][j];

@@ -397,11 +397,8 @@ hipError_t gemm_run(const GemmDesc& d, float* ws, size_t ws_elems, hipStream_t s
     p.C = d.C; p.ldc = d.ldc; p.sC = d.sC;
     if (d.valu) return gemm_valu_launch(p, d, d.epi.mode, st);
     if (d.prec != GEMM_F32) {
-      // BCE with a bf16-plane target: two launches, each running only for its *xdyn state
-      if (d.epi.mode == EPI_BCE && d.epi.xp && d.epi.xdyn) {
-        hipError_t e = gemm_bf16_launch(p, d, EPI_BCE, st);
-        return e != hipSuccess ? e : gemm_bf16_launch(p, d, EPI_BCEB, st);
-      }
+      // BCE with a bf16-plane target: one launch choosing the plane or the fp32 target by *xdyn
+      if (d.epi.mode == EPI_BCE && d.epi.xp && d.epi.xdyn) return gemm_bf16_launch(p, d, EPI_BCEB, st);
       Params q = p;
       q.epi.xdyn = nullptr;  // a single BCE launch always runs (fp32 target)
       return gemm_bf16_launch(q, d, d.epi.mode, st);

@@ -5,7 +5,8 @@
 # (the revision is checked out as a worktree in .wt_head, listed in .gitignore / .gpurunignore)
 set -e
 cd "$(dirname "$0")/.."
-REV=$1; OUT=$2
+# (the revision resolved HERE: inside the worktree "HEAD" would name the worktree's own checkout)
+REV=$(git rev-parse --verify "$1^{commit}"); OUT=$2
 H=$(python3 -c "import magic_amd.build as b; print(b.source_hash())")
 if [ -d .wt_head ]; then git -C .wt_head checkout -q --detach "$REV"; else git worktree add -f .wt_head "$REV" -q --detach; fi
 (cd .wt_head && python3 -c "
