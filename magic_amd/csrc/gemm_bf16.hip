@@ -785,9 +785,10 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   if (!p.dyn) p.npairs0 = n;
   p.pab = 0;
   for (int i = 0; i < n; ++i) p.pab |= (p.pa[i] | p.pb[i] << 2) << (4 * i);
-  // the eight-phase kernel's image-reusing walk (plane pairs only). Not on the BCE head: its
-  // whole-round launch and its 256x128 ring-tile remainder (bce_split) must sum alike
-  p.reuse = n > 1 && d.epi.mode != EPI_BCE && d.epi.mode != EPI_BCEB;
+  // the eight-phase kernel's image-reusing walk (plane pairs only; the BCE head's whole-round
+  // launch then sums in another order than its 256x128 ring-tile remainder, bce_split: the same
+  // values to fp32 rounding)
+  p.reuse = n > 1;
   if (gemm_bf16_wide(d)) {
     // tile N: the planner's (gemm_run), 256 for the diagnostic variants of the 256x256 forms
     const bool q = d.variant == 0 || d.variant == 3 || d.variant == 6 || (d.variant >= 10 && d.variant <= 15);

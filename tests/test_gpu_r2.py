@@ -341,10 +341,12 @@ def test_early_adam_is_bitwise_identical(prec):
 
 
 @pytest.mark.parametrize("prec", ["f32x", "bf16"])
-def test_bce_split_is_bitwise_identical(prec):
+def test_bce_split_matches_one_launch(prec):
     """The BCE head in whole rounds plus 256x128 ring tiles for the remaining columns (option
     bce_split; 66 x 66 images, B = 4096: 16 x 18 = 288 tiles of 256x256 -> 16 n-tiles + 272
-    columns) vs one launch: bitwise identical losses, distance and gradients."""
+    columns) vs one launch: bitwise identical in bf16; in f32x the eight-phase kernel's
+    image-reusing walk sums the plane pairs in another order than the ring kernel, so the
+    remainder columns agree to fp32 rounding (losses, distance and gradients within 1e-6)."""
     cfg = preset("8c", image_size=66, batch=4096, precision=prec).replace(enc=(300, 260))
     P = make_params(cfg)
     X, areas, eps = make_inputs(cfg, cfg.batch)
@@ -355,11 +357,17 @@ def test_bce_split_is_bitwise_identical(prec):
             eng.set_option("bce_split", split)
             eng.load_params(P)
             outs.append(gpu_phases(eng, X, areas, eps))
+        def same(u, v):
+            if prec == "bf16":
+                np.testing.assert_array_equal(u, v)
+            else:
+                u, v = np.asarray(u, np.float64), np.asarray(v, np.float64)
+                assert np.abs(u - v).max() <= 1e-6 * max(np.abs(v).max(), 1e-30)
         for u, v in zip(outs[0][:2], outs[1][:2]):
-            np.testing.assert_array_equal(u, v)
+            same(u, v)
         for d in (2, 3):
             for k in outs[0][d]:
-                np.testing.assert_array_equal(outs[0][d][k], outs[1][d][k])
+                same(outs[0][d][k], outs[1][d][k])
     finally:
         eng.close()
 

@@ -1,17 +1,12 @@
 #!/bin/bash
 # The current GPU session (overwritten per session; earlier sessions are in git history):
 #   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r5zc: the round's last changes, each against its parent commit (tools/build_rev.sh resolved
-# "HEAD" inside its worktree until now, so the r5q-r5zb baselines were all commit e10f80b):
-# libraries of 69aa44a (enc chain), 3f00a78 (+ BCE target bits), 590d7a3 (+ reuse walk), 91b90f1
-# (+ one join), d856703 (+ events without system fence) and this tree (+ one BCE launch),
-# rotated in that order, two rounds each of C2 and C3 (100 steps).
+# r5ze: the eight-phase image-reusing walk on the f32x BCE head too (bce_split's remainder then
+# agrees to fp32 rounding instead of bitwise): tests, then C2 against HEAD's library, alternating.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 100"
-r() { echo "r5zc_$1|120|$3 python bench.py --config $2 $BQ > gpurun_out/r5zc_$1.json"; }
-rot() {  # config round
-  for v in chain bits reuse join ev; do echo "$(r ${1}_${v}$2 $1 MVAE_LIB=magic_amd/libmvae_$v.so)"; done
-  echo "$(r ${1}_tree$2 $1)"
-}
-mapfile -t S < <(rot C2 1; rot C3 1; rot C2 2; rot C3 2)
-bash tools/gpu_steps.sh "${S[@]}"
+r() { echo "r5ze_$1|120|$3 python bench.py --config $2 $BQ > gpurun_out/r5ze_$1.json"; }
+H="MVAE_LIB=magic_amd/libmvae_head.so"
+bash tools/gpu_steps.sh \
+  "r5ze_t|600|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_r2.py tests/test_gpu_parity.py tests/test_gpu_golden.py" \
+  "$(r c2_h1 C2 "$H")" "$(r c2_n1 C2)" "$(r c2_h2 C2 "$H")" "$(r c2_n2 C2)" "$(r c2_h3 C2 "$H")" "$(r c2_n3 C2)"
