@@ -1,12 +1,10 @@
 #!/bin/bash
 # The current GPU session (overwritten per session; earlier sessions are in git history):
 #   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r5ze: the eight-phase image-reusing walk on the f32x BCE head too (bce_split's remainder then
-# agrees to fp32 rounding instead of bitwise): tests, then C2 against HEAD's library, alternating.
+# r5zg: C2's f32x hidden / decoder GEMMs (with their step epilogues, outputs as planes) on the
+# planner's kernel (32) vs the eight-phase kernel forced (45: with the image-reusing walk) and its
+# planner split -- the planner's e8 rule predates the walk.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 100"
-r() { echo "r5ze_$1|120|$3 python bench.py --config $2 $BQ > gpurun_out/r5ze_$1.json"; }
-H="MVAE_LIB=magic_amd/libmvae_head.so"
+S="enc_fwd_h,enc_bwd_d_h,enc_bwd_w_h,dec_fwd_2,dec_bwd_d_2,dec_bwd_w_2,enc_fwd_0,enc_bwd_w_0,dec_fwd_out,dec_bwd_d_out,dec_bwd_w_out"
 bash tools/gpu_steps.sh \
-  "r5ze_t|600|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_r2.py tests/test_gpu_parity.py tests/test_gpu_golden.py" \
-  "$(r c2_h1 C2 "$H")" "$(r c2_n1 C2)" "$(r c2_h2 C2 "$H")" "$(r c2_n2 C2)" "$(r c2_h3 C2 "$H")" "$(r c2_n3 C2)"
+  "r5zg|300|MVAE_BENCH_PLANES_ONLY=1 python tools/gemm_bench.py --config C2 --variants 32,45 --rounds 5 --epilogues --shapes $S"
