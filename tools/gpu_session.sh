@@ -1,10 +1,17 @@
 #!/bin/bash
 # The current GPU session (overwritten per session; earlier sessions are in git history):
 #   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r5zg: C2's f32x hidden / decoder GEMMs (with their step epilogues, outputs as planes) on the
-# planner's kernel (32) vs the eight-phase kernel forced (45: with the image-reusing walk) and its
-# planner split -- the planner's e8 rule predates the walk.
+# r5zh: verification of the tree: full GPU suite, smoke, the default bench line (CPU baseline + PMC
+# traffic + configs block), per-config rocprofv3 kernel-trace runs (C2, C3, C5).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-S="enc_fwd_h,enc_bwd_d_h,enc_bwd_w_h,dec_fwd_2,dec_bwd_d_2,dec_bwd_w_2,enc_fwd_0,enc_bwd_w_0,dec_fwd_out,dec_bwd_d_out,dec_bwd_w_out"
+export TMPDIR=/tmp
+PT="python -u -m pytest -q --maxfail=10 --timeout 120 --timeout-method thread -p no:cacheprovider"
+RP="rocprofv3 --kernel-trace --stats -f csv"
+BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 10 --warmup 3"
 bash tools/gpu_steps.sh \
-  "r5zg|300|MVAE_BENCH_PLANES_ONLY=1 python tools/gemm_bench.py --config C2 --variants 32,45 --rounds 5 --epilogues --shapes $S"
+  "r5zh_tests|400|$PT tests -m gpu" \
+  "r5zh_smoke|120|python -c 'import __graft_entry__ as g; g.smoke()'" \
+  "r5zh_bench|500|python bench.py > gpurun_out/r5zh_bench.json 2> gpurun_out/r5zh_bench.err" \
+  "r5zh_prof_c2|150|$RP -d gpurun_out/r5zh_prof_c2 -o c2 -- python bench.py --config C2 $BQ" \
+  "r5zh_prof_c3|150|$RP -d gpurun_out/r5zh_prof_c3 -o c3 -- python bench.py --config C3 $BQ" \
+  "r5zh_prof_c5|150|$RP -d gpurun_out/r5zh_prof_c5 -o c5 -- python bench.py --config C5 $BQ"
