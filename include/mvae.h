@@ -189,7 +189,9 @@ int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* cou
  * all-reduce): the caller's stream then joins the side stream in mvae_adam;
  * mvae_train_step uses it in the bf16 and f32x modes; "bce_split" (default 1) runs a BCE head whose
  * 256x256 tiles leave a partial last round as the whole rounds plus 256x128 tiles for the rest
- * (the same results). */
+ * (the same results); "side_mask" (0-3, default 3): which weight gradients run on the side
+ * stream -- bit 0 the decoder's, bit 1 the encoder's (a cleared bit: in order on the caller's
+ * stream; the same results). */
 int mvae_set_option(mvae_ctx* ctx, const char* name, int value);
 /* Both TF ApplyAdam updates from MVAE_BUF_GRADS (theta -= d1(g1) + d2(g2)).           */
 int mvae_adam(mvae_ctx* ctx, void* stream);

@@ -105,6 +105,8 @@ struct mvae_ctx {
   bool early_adam = false;   // option "early_adam": Adam of the parameters after the layer-0
                              // block runs on the side stream beside the layer-0 weight gradient
   bool early_fork = false;   // ... the side stream waits for the dgrad chain this step
+  int side_mask = 3;         // option "side_mask": weight gradients on the side stream -- bit 0
+                             // the decoder's, bit 1 the encoder's (else in order on the caller's)
   bool valu = true;          // skinny GEMMs on the fp32 VALU kernel (env MVAE_NO_VALU=1: off)
   std::vector<void*> allocs;
   // bf16 plane images (bf16 / f32x modes): fp32 buffer -> planes of the same layout
@@ -1317,16 +1319,21 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
   };
   if (part == 0) {
     // bwd_dec: W_out, D_out, W_d2, D_d2, W_d1, D_z
-    if ((rc = fork())) return rc;
-    c->side_pending = two;
-    if ((rc = run(c, c->bwd_dec[0], sd, c->bwd_dec_r[0]))) return rc;
-    if ((rc = run(c, c->bwd_dec[1], st, c->bwd_dec_r[1]))) return rc;
-    if ((rc = fork())) return rc;
-    if ((rc = run(c, c->bwd_dec[2], sd, c->bwd_dec_r[2]))) return rc;
-    if ((rc = run(c, c->bwd_dec[3], st, c->bwd_dec_r[3]))) return rc;
-    if ((rc = fork())) return rc;
-    if ((rc = run(c, c->bwd_dec[4], sd, c->bwd_dec_r[4]))) return rc;
-    if ((rc = run(c, c->bwd_dec[5], st, c->bwd_dec_r[5]))) return rc;
+    if (!(c->side_mask & 1)) {  // option side_mask: the decoder's weight gradients in order here
+      for (int i = 0; i < 6; ++i)
+        if ((rc = run(c, c->bwd_dec[i], st, c->bwd_dec_r[i]))) return rc;
+    } else {
+      if ((rc = fork())) return rc;
+      c->side_pending = two;
+      if ((rc = run(c, c->bwd_dec[0], sd, c->bwd_dec_r[0]))) return rc;
+      if ((rc = run(c, c->bwd_dec[1], st, c->bwd_dec_r[1]))) return rc;
+      if ((rc = fork())) return rc;
+      if ((rc = run(c, c->bwd_dec[2], sd, c->bwd_dec_r[2]))) return rc;
+      if ((rc = run(c, c->bwd_dec[3], st, c->bwd_dec_r[3]))) return rc;
+      if ((rc = fork())) return rc;
+      if ((rc = run(c, c->bwd_dec[4], sd, c->bwd_dec_r[4]))) return rc;
+      if ((rc = run(c, c->bwd_dec[5], st, c->bwd_dec_r[5]))) return rc;
+    }
     if (join_dec && (rc = join())) return rc;
   } else if (part == 1) {
     {
@@ -1340,15 +1347,19 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
     // produces dZ_{i-1}, wgrad(i) needs dZ_i (dgrad(n) = the head's: dZ of layer n-1)
     auto wg = [&](int i) -> const GemmDesc& { return c->bwd_enc[c->enc_part1 + (n - i)]; };
     auto wr = [&](int i) { return c->bwd_enc_r[c->enc_part1 + (n - i)]; };
-    if ((rc = fork())) return rc;
-    c->side_pending = two;
-    if ((rc = run(c, wg(n), sd, wr(n)))) return rc;  // head weight gradient (dhead)
+    const bool es = (c->side_mask & 2) != 0;  // the encoder's weight gradients on the side stream
+    hipStream_t se = es ? sd : st;
+    if (es) {
+      if ((rc = fork())) return rc;
+      c->side_pending = two;
+    }
+    if ((rc = run(c, wg(n), se, wr(n)))) return rc;  // head weight gradient (dhead)
     for (int j = 0; j < n; ++j) {
       const int i = n - j;  // dgrad(i) -> dZ_{i-1}
       if ((rc = run(c, c->bwd_enc[j], st, c->bwd_enc_r[j]))) return rc;
       if (i - 1 >= 1) {
-        if ((rc = fork())) return rc;
-        if ((rc = run(c, wg(i - 1), sd, wr(i - 1)))) return rc;
+        if (es && (rc = fork())) return rc;
+        if ((rc = run(c, wg(i - 1), se, wr(i - 1)))) return rc;
       }
     }
     // early Adam: the side stream's Adam of the blocks after layer 0 (mvae_adam) may start once
@@ -1408,6 +1419,12 @@ extern "C" int mvae_set_option(mvae_ctx* ctx, const char* name, int value) {
   }
   if (k == "bce_split") {
     ctx->use_split = value != 0;
+    return MVAE_OK;
+  }
+  if (k == "side_mask") {
+    if (value < 0 || value > 3) return fail(ctx, MVAE_EINVAL, "side_mask must be in [0, 3]");
+    if (ctx->phase == 4) return fail(ctx, MVAE_ESTATE, "side_mask cannot change mid-backward");
+    ctx->side_mask = value;
     return MVAE_OK;
   }
   if (k == "early_adam") {

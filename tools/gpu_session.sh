@@ -1,17 +1,12 @@
 #!/bin/bash
 # The current GPU session (overwritten per session; earlier sessions are in git history):
 #   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r5zh: verification of the tree: full GPU suite, smoke, the default bench line (CPU baseline + PMC
-# traffic + configs block), per-config rocprofv3 kernel-trace runs (C2, C3, C5).
+# r5zj: which weight gradients gain from the side stream: option side_mask 3 (default: decoder and
+# encoder wgrads beside the dgrad chains), 2 (decoder's in order on the main stream), 1 (encoder's
+# in order), 0 (both), alternating, C2 / C3 / C5.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export TMPDIR=/tmp
-PT="python -u -m pytest -q --maxfail=10 --timeout 120 --timeout-method thread -p no:cacheprovider"
-RP="rocprofv3 --kernel-trace --stats -f csv"
-BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 10 --warmup 3"
-bash tools/gpu_steps.sh \
-  "r5zh_tests|400|$PT tests -m gpu" \
-  "r5zh_smoke|120|python -c 'import __graft_entry__ as g; g.smoke()'" \
-  "r5zh_bench|500|python bench.py > gpurun_out/r5zh_bench.json 2> gpurun_out/r5zh_bench.err" \
-  "r5zh_prof_c2|150|$RP -d gpurun_out/r5zh_prof_c2 -o c2 -- python bench.py --config C2 $BQ" \
-  "r5zh_prof_c3|150|$RP -d gpurun_out/r5zh_prof_c3 -o c3 -- python bench.py --config C3 $BQ" \
-  "r5zh_prof_c5|150|$RP -d gpurun_out/r5zh_prof_c5 -o c5 -- python bench.py --config C5 $BQ"
+BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 100"
+r() { echo "r5zj_$1|120|python bench.py --config $2 $BQ $3 > gpurun_out/r5zj_$1.json"; }
+rot() { for m in 3 2 1 0; do echo "$(r ${1}_m${m}$2 $1 "--opt side_mask=$m")"; done; }
+mapfile -t S < <(rot C2 1; rot C3 1; rot C5 1; rot C2 2; rot C3 2)
+bash tools/gpu_steps.sh "${S[@]}"
