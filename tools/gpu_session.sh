@@ -1,12 +1,15 @@
 #!/bin/bash
 # The current GPU session (overwritten per session; earlier sessions are in git history):
 #   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r5zj: which weight gradients gain from the side stream: option side_mask 3 (default: decoder and
-# encoder wgrads beside the dgrad chains), 2 (decoder's in order on the main stream), 1 (encoder's
-# in order), 0 (both), alternating, C2 / C3 / C5.
+# r5zk: with the early Adam, the layer-0 weight gradient's split-K reduction applies the layer-0
+# block's Adam updates itself (launch_splitk_adam): tests (early Adam bitwise vs one Adam launch,
+# DP, parity, golden), then C2 / C3 / C5 against the parent commit's library, alternating.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 100"
-r() { echo "r5zj_$1|120|python bench.py --config $2 $BQ $3 > gpurun_out/r5zj_$1.json"; }
-rot() { for m in 3 2 1 0; do echo "$(r ${1}_m${m}$2 $1 "--opt side_mask=$m")"; done; }
-mapfile -t S < <(rot C2 1; rot C3 1; rot C5 1; rot C2 2; rot C3 2)
-bash tools/gpu_steps.sh "${S[@]}"
+r() { echo "r5zk_$1|120|$3 python bench.py --config $2 $BQ > gpurun_out/r5zk_$1.json"; }
+H="MVAE_LIB=magic_amd/libmvae_head.so"
+bash tools/gpu_steps.sh \
+  "r5zk_t|600|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_r2.py tests/test_gpu_dp.py tests/test_gpu_parity.py tests/test_gpu_golden.py" \
+  "$(r c2_h1 C2 "$H")" "$(r c2_n1 C2)" "$(r c2_h2 C2 "$H")" "$(r c2_n2 C2)" \
+  "$(r c3_h1 C3 "$H")" "$(r c3_n1 C3)" "$(r c3_h2 C3 "$H")" "$(r c3_n2 C3)" \
+  "$(r c5_h1 C5 "$H")" "$(r c5_n1 C5)" "$(r c5_h2 C5 "$H")" "$(r c5_n2 C5)"
