@@ -132,6 +132,7 @@ def region_flops(cfg, name: str) -> float:
     table = {
         "head_fwd": 2.0 * 3 * B * e * 2 * L,
         "dec_fwd_1": 2.0 * B * L * d0, "dec_fwd_2": 2.0 * B * d0 * d1,
+        "dec_fwd_chain": 2.0 * B * L * d0 + 2.0 * B * d0 * d1,  # both hidden layers, one launch
         "dec_fwd_out_bce": 2.0 * B * d1 * D,
         "dec_bwd_w_out": 2.0 * B * d1 * D, "dec_bwd_d_out": 2.0 * B * D * d1,
         "dec_bwd_w_2": 2.0 * B * d0 * d1, "dec_bwd_d_2": 2.0 * B * d0 * d1,

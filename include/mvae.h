@@ -128,7 +128,8 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out);
  * valu (0/1), dact_planes (0/1), bce_split (0/1), plan_log (0/1: GEMM plans on stderr),
  * conv2_half (0/1), conv2_nw (4/8/16), conv2_tpb (1/2), conv2_fpw (2/4), conv2_wg (4/8),
  * conv2_nchunk (> 0), enc_chain (0/1: bf16 mode, the encoder's hidden layers in one launch,
- * default 1), enc_chain_rows (its rows per workgroup, 16..96; 0 auto). Diagnostics, results
+ * default 1), enc_chain_rows (its rows per workgroup, 16..96; 0 auto; both chains), dec_chain
+ * (0/1: bf16 mode, the decoder's two hidden layers in one launch, default 1). Diagnostics, results
  * meaningless: diag_skip_deint (1: de-interleave only the first batch -- a timing bound),
  * diag_shadow_deint (-1 or a workgroup count > 0: a second de-interleave of each step's input
  * into a scratch image on a low-priority stream, launched at diag_shadow_at = 0 the forward,

@@ -126,6 +126,10 @@ struct mvae_ctx {
   ChainArgs chain_args;
   int chain_r = 0;
   GemmDesc f_d1, f_d2, f_out;
+  // the decoder's hidden layers f_d1, f_d2 as one launch (the same kernel; option dec_chain)
+  bool dchain = false;
+  ChainArgs dchain_args;
+  int dchain_r = 0;
   GemmDesc f_out_a, f_out_b;  // f_out as whole rounds of 256x256 tiles + the rest (f_split)
   bool f_split = false;
   bool use_split = true;      // option "bce_split" (default 1)
@@ -430,6 +434,7 @@ struct CreateOpts {
   int enc_chain = 1;    // bf16 mode: the encoder's hidden layers in one launch (0: one GEMM each)
   int enc_chain_rows = 0;  // ... its rows per workgroup forced (16..96, multiple of 16; 0 auto)
   int diag_chain = 0;      // ... its timing ablations (ChainArgs::diag; results meaningless)
+  int dec_chain = 1;    // bf16 mode: the decoder's two hidden layers in one launch (0: one GEMM each)
   int conv2_nw = 8, conv2_tpb = 1, conv2_fpw = 2, conv2_wg = 8, conv2_half = 1, conv2_nchunk = 0;
 };
 
@@ -461,6 +466,7 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "diag_shadow_at" && in(0, 2)) o->diag_shadow_at = (int)v;
     else if (k == "enc_chain" && in(0, 1)) o->enc_chain = (int)v;
     else if (k == "diag_chain" && in(0, 7)) o->diag_chain = (int)v;
+    else if (k == "dec_chain" && in(0, 1)) o->dec_chain = (int)v;
     else if (k == "enc_chain_rows" && (v == 0 || (in(16, 96) && v % 16 == 0))) o->enc_chain_rows = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
     else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
@@ -863,28 +869,43 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
   c->ws_elems = ws;
   // the hidden encoder layers as one launch: bf16 planes in and out, tanh / elu epilogues writing
   // planes only, widths that fit the kernel's 512-column activation block
-  if (opt.enc_chain && c->np == 1 && c->nenc >= 3 && c->nenc - 1 <= 4) {
-    bool ok = true;
-    ChainArgs& ca = c->chain_args;
-    ca.x = c->fwd_enc[1].Ap;
-    ca.ldx = c->fwd_enc[1].lda;
-    ca.M = c->fwd_enc[1].M;
-    ca.nl = c->nenc - 1;
-    ca.act = c->fwd_enc[1].epi.act;
+  // hidden layers as one launch (enc_chain.hip): bf16 planes in and out, tanh / elu epilogues
+  // writing planes only, widths that fit the kernel's 512-column activation block; ds[i] reads
+  // ds[i - 1]'s output plane
+  auto chain_of = [&](std::initializer_list<const GemmDesc*> ds, ChainArgs& ca) {
+    const GemmDesc& d0 = **ds.begin();
+    ca.x = d0.Ap;
+    ca.ldx = d0.lda;
+    ca.M = d0.M;
+    ca.nl = (int)ds.size();
+    ca.act = d0.epi.act;
     ca.rows = opt.enc_chain_rows;
     ca.diag = opt.diag_chain;
-    for (int i = 1; i < c->nenc; ++i) {
-      const GemmDesc& d = c->fwd_enc[i];
+    bool ok = ca.nl >= 1 && ca.nl <= 4;
+    const GemmDesc* prev = nullptr;
+    int i = 0;
+    for (const GemmDesc* p : ds) {
+      if (i >= 4) break;
+      const GemmDesc& d = *p;
       ok = ok && d.prec == GEMM_BF16 && !d.valu && d.epi.mode == EPI_ACT && d.epi.c32 == 0 &&
            d.epi.cp && d.epi.ncp == 1 && d.epi.padw == 2 && d.Ap && d.Bp && d.batch == 1 && !d.at &&
            !d.bt && d.K <= 512 && d.N <= 511 && d.M == ca.M && d.epi.act == ca.act;
-      ChainLayer& cl = ca.l[i - 1];
+      ChainLayer& cl = ca.l[i++];
       cl.w = d.Bp; cl.ldw = d.ldb; cl.K = d.K; cl.N = d.N; cl.out = d.epi.cp; cl.ldo = d.ldc;
-      if (i > 1) ok = ok && d.Ap == c->fwd_enc[i - 1].epi.cp && d.lda == c->fwd_enc[i - 1].ldc;
+      if (prev) ok = ok && d.Ap == prev->epi.cp && d.lda == prev->ldc;
+      prev = p;
     }
-    c->chain = ok;
-    c->chain_r = region(c, "enc_fwd_chain");
-  }
+    return ok;
+  };
+  if (opt.enc_chain && c->np == 1 && c->nenc == 3)
+    c->chain = chain_of({&c->fwd_enc[1], &c->fwd_enc[2]}, c->chain_args);
+  else if (opt.enc_chain && c->np == 1 && c->nenc == 4)
+    c->chain = chain_of({&c->fwd_enc[1], &c->fwd_enc[2], &c->fwd_enc[3]}, c->chain_args);
+  else if (opt.enc_chain && c->np == 1 && c->nenc == 5)
+    c->chain = chain_of({&c->fwd_enc[1], &c->fwd_enc[2], &c->fwd_enc[3], &c->fwd_enc[4]}, c->chain_args);
+  if (c->chain) c->chain_r = region(c, "enc_fwd_chain");
+  if (opt.dec_chain && c->np == 1) c->dchain = chain_of({&c->f_d1, &c->f_d2}, c->dchain_args);
+  if (c->dchain) c->dchain_r = region(c, "dec_fwd_chain");
   if (opt.plan_log) {
     // the GEMM plans of this context (diagnostics): shape, arithmetic, kernel, split-K + combine
     auto show = [&](const GemmDesc& d, int r) {
@@ -899,6 +920,9 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
       std::fprintf(stderr, "[mvae plan] enc_fwd_chain    layers 1..%d in one launch, %d rows per workgroup\n",
                    c->nenc - 1, enc_chain_rows(c->chain_args.M, c->chain_args.rows));
     show(c->f_d1, c->f_d1_r); show(c->f_d2, c->f_d2_r); show(c->f_out, c->f_out_r);
+    if (c->dchain)
+      std::fprintf(stderr, "[mvae plan] dec_fwd_chain    f_d1, f_d2 in one launch, %d rows per workgroup\n",
+                   enc_chain_rows(c->dchain_args.M, c->dchain_args.rows));
     for (size_t i = 0; i < c->bwd_dec.size(); ++i) show(c->bwd_dec[i], c->bwd_dec_r[i]);
     for (size_t i = 0; i < c->bwd_enc.size(); ++i) show(c->bwd_enc[i], c->bwd_enc_r[i]);
   }
@@ -1206,13 +1230,23 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
   return MVAE_OK;
 }
 
+// the decoder's hidden layers: one chain launch or one GEMM each
+static int decode_hidden(mvae_ctx* ctx, hipStream_t st) {
+  if (ctx->dchain) {
+    TimeScope ts(ctx, ctx->dchain_r, st);
+    MV_CHECK(launch_enc_chain(ctx->dchain_args, st));
+    return MVAE_OK;
+  }
+  int rc = run(ctx, ctx->f_d1, st, ctx->f_d1_r);
+  return rc ? rc : run(ctx, ctx->f_d2, st, ctx->f_d2_r);
+}
+
 extern "C" int mvae_forward(mvae_ctx* ctx, const float* x, const float* eps, void* stream) {
   if (!ctx || !x) return MVAE_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   int rc = encode(ctx, x, eps, st);
   if (rc) return rc;
-  if ((rc = run(ctx, ctx->f_d1, st, ctx->f_d1_r))) return rc;
-  if ((rc = run(ctx, ctx->f_d2, st, ctx->f_d2_r))) return rc;
+  if ((rc = decode_hidden(ctx, st))) return rc;
   if (ctx->f_split && ctx->use_split) {
     if ((rc = run(ctx, ctx->f_out_a, st, ctx->f_out_r))) return rc;
     if ((rc = run(ctx, ctx->f_out_b, st, ctx->f_out_r))) return rc;
@@ -1580,8 +1614,7 @@ extern "C" int mvae_reconstruct(mvae_ctx* ctx, const float* x, const float* eps,
   hipStream_t st = (hipStream_t)stream;
   int rc = encode(ctx, x, eps, st, ENC_EVAL);
   if (rc) return rc;
-  if ((rc = run(ctx, ctx->f_d1, st))) return rc;
-  if ((rc = run(ctx, ctx->f_d2, st))) return rc;
+  if ((rc = decode_hidden(ctx, st))) return rc;
   GemmDesc d = ctx->f_out;
   d.epi.y = y_out;
   d.epi.ldy = ctx->D;

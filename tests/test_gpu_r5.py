@@ -1,6 +1,7 @@
-"""GPU parity for round 5's fused encoder chain (enc_chain.hip): the bf16 encoder's hidden layers
-in one launch, activation block resident in LDS, against the float64 oracle at the documented bf16
-bar and against the per-layer GEMMs it replaces (create option enc_chain=0)."""
+"""GPU parity for round 5's fused hidden-layer chains (enc_chain.hip): the bf16 encoder's and
+decoder's hidden layers in one launch each, activation block resident in LDS, against the float64
+oracle at the documented bf16 bar and against the per-layer GEMMs they replace (create options
+enc_chain=0 / dec_chain=0)."""
 import numpy as np
 import pytest
 import torch
@@ -21,7 +22,7 @@ def _need_gpu():
 
 
 @pytest.mark.parametrize("opts", ["enc_chain=1", "enc_chain=0", "enc_chain_rows=32", "enc_chain_rows=64",
-                                  "enc_chain_rows=96"])
+                                  "enc_chain_rows=96", "dec_chain=0", "enc_chain=0,dec_chain=0"])
 def test_enc_chain_step_c3_shape(opts):
     """C3's encoder (4 x 500, tanh) at B = 2048: 6144 rows, 16 rows per workgroup (auto), and
     forced 32 / 64 / 96-row blocks (four, three and two weight steps in LDS)."""
@@ -35,6 +36,39 @@ def test_enc_chain_step_widths(enc, act, batch):
     layers, elu, and row counts that leave the last workgroup's block partly past M."""
     cfg = preset("8d", image_size=24, batch=batch, precision="bf16").replace(enc=enc, act=act, latent=16)
     check_step(cfg, adam=False, **BF16)
+
+
+@pytest.mark.parametrize("latent,dec,act,batch", [(200, (500, 500), "tanh", 4096), (16, (400, 300), "elu", 100),
+                                                  (31, (511, 200), "tanh", 37), (8, (64, 500), "tanh", 1000)])
+def test_dec_chain_step(latent, dec, act, batch):
+    """The decoder's two hidden layers in one launch (option dec_chain, default on in bf16 mode):
+    C3's decoder, ragged latent / hidden widths (511: the ones column is the block's last), elu,
+    and row counts that leave the last workgroup's block partly past B."""
+    cfg = preset("8d", image_size=24, batch=batch, precision="bf16").replace(latent=latent, dec=dec, act=act)
+    check_step(cfg, adam=False, **BF16)
+
+
+def _recon(cfg, X):
+    from magic_amd.engine import Engine
+    eng = Engine(cfg, 0)
+    try:
+        eng.load_params(make_params(cfg))
+        out = eng.reconstruct(to_dev(X))
+        torch.cuda.synchronize()
+        return out.cpu().numpy().astype(np.float64)
+    finally:
+        eng.close()
+
+
+def test_dec_chain_matches_per_layer_gemms():
+    """Reconstructions at C3's full shape: the decoder chain against one GEMM per hidden layer
+    (the same bf16 arithmetic, another accumulation order)."""
+    cfg = baseline_config("C3")
+    X, _, _ = make_inputs(cfg, cfg.batch, seed=5)
+    a = _recon(cfg.replace(options="dec_chain=1"), X)
+    b = _recon(cfg.replace(options="dec_chain=0"), X)
+    assert np.all(np.isfinite(a))
+    assert np.abs(a - b).max() <= 2e-2
 
 
 def _means(cfg, X):

@@ -1,15 +1,12 @@
 #!/bin/bash
 # The current GPU session (overwritten per session; earlier sessions are in git history):
 #   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r5zk: with the early Adam, the layer-0 weight gradient's split-K reduction applies the layer-0
-# block's Adam updates itself (launch_splitk_adam): tests (early Adam bitwise vs one Adam launch,
-# DP, parity, golden), then C2 / C3 / C5 against the parent commit's library, alternating.
+# r5zm: the decoder's two hidden layers in one enc_chain launch (create option dec_chain): the
+# A/B (r5zl ran the plan and the tests: 472 passed): C3 / C5 against the parent commit's library.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 100"
-r() { echo "r5zk_$1|120|$3 python bench.py --config $2 $BQ > gpurun_out/r5zk_$1.json"; }
+r() { echo "r5zm_$1|120|$3 python bench.py --config $2 $BQ > gpurun_out/r5zm_$1.json"; }
 H="MVAE_LIB=magic_amd/libmvae_head.so"
 bash tools/gpu_steps.sh \
-  "r5zk_t|600|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_r2.py tests/test_gpu_dp.py tests/test_gpu_parity.py tests/test_gpu_golden.py" \
-  "$(r c2_h1 C2 "$H")" "$(r c2_n1 C2)" "$(r c2_h2 C2 "$H")" "$(r c2_n2 C2)" \
-  "$(r c3_h1 C3 "$H")" "$(r c3_n1 C3)" "$(r c3_h2 C3 "$H")" "$(r c3_n2 C3)" \
+  "$(r c3_h1 C3 "$H")" "$(r c3_n1 C3)" "$(r c3_h2 C3 "$H")" "$(r c3_n2 C3)" "$(r c3_h3 C3 "$H")" "$(r c3_n3 C3)" \
   "$(r c5_h1 C5 "$H")" "$(r c5_n1 C5)" "$(r c5_h2 C5 "$H")" "$(r c5_n2 C5)"
