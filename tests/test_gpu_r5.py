@@ -29,12 +29,16 @@ def test_enc_chain_step_c3_shape(opts):
     check_step(baseline_config("C3").replace(batch=2048, options=opts), adam=False, **BF16)
 
 
-@pytest.mark.parametrize("enc,act,batch", [((400, 300, 260), "elu", 100), ((500, 500, 500, 500, 300), "tanh", 50),
-                                           ((300, 200, 511), "tanh", 37)])
-def test_enc_chain_step_widths(enc, act, batch):
+@pytest.mark.parametrize("enc,act,batch,latent", [((400, 300, 260), "elu", 100, 16),
+                                                  ((500, 500, 500, 500, 300), "tanh", 50, 16),
+                                                  ((300, 200, 511), "tanh", 37, 16), ((300, 200, 511), "tanh", 37, 250),
+                                                  ((500, 500, 500, 500), "tanh", 64, 255),
+                                                  ((500, 500, 500, 500, 300, 200), "elu", 40, 20)])
+def test_enc_chain_step_widths(enc, act, batch, latent):
     """Ragged widths (a 511-wide hidden layer: its ones column is the block's last), four fused
-    layers, elu, and row counts that leave the last workgroup's block partly past M."""
-    cfg = preset("8d", image_size=24, batch=batch, precision="bf16").replace(enc=enc, act=act, latent=16)
+    layers, five (no chain), 500 / 510-column latent heads after the chain, elu, and row counts
+    that leave the last workgroup's block partly past M."""
+    cfg = preset("8d", image_size=24, batch=batch, precision="bf16").replace(enc=enc, act=act, latent=latent)
     check_step(cfg, adam=False, **BF16)
 
 
