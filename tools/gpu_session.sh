@@ -1,14 +1,17 @@
 #!/bin/bash
 # The current GPU session (overwritten per session; earlier sessions are in git history):
 #   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r5zn: the latent head as the encoder chain's last, linear layer (fp32 rows of ms; create option
-# head_chain): the plan at C3, chain tests + parity / golden / r2, then C3 / C5 against the parent.
+# r5zo: verification of the tree after the decoder chain: full GPU suite, smoke, the default bench line (CPU baseline + PMC
+# traffic + configs block), per-config rocprofv3 kernel-trace runs (C2, C3, C5).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 100"
-r() { echo "r5zn_$1|120|$3 python bench.py --config $2 $BQ > gpurun_out/r5zn_$1.json"; }
-H="MVAE_LIB=magic_amd/libmvae_head.so"
+export TMPDIR=/tmp
+PT="python -u -m pytest -q --maxfail=10 --timeout 120 --timeout-method thread -p no:cacheprovider"
+RP="rocprofv3 --kernel-trace --stats -f csv"
+BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 10 --warmup 3"
 bash tools/gpu_steps.sh \
-  "r5zn_plan|120|python bench.py --config C3 $BQ --steps 3 --create-opt plan_log=1 > gpurun_out/r5zn_plan.json" \
-  "r5zn_t|600|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_r5.py tests/test_gpu_parity.py tests/test_gpu_golden.py tests/test_gpu_r2.py" \
-  "$(r c3_h1 C3 "$H")" "$(r c3_n1 C3)" "$(r c3_h2 C3 "$H")" "$(r c3_n2 C3)" "$(r c3_h3 C3 "$H")" "$(r c3_n3 C3)" \
-  "$(r c5_h1 C5 "$H")" "$(r c5_n1 C5)" "$(r c5_h2 C5 "$H")" "$(r c5_n2 C5)"
+  "r5zo_tests|400|$PT tests -m gpu" \
+  "r5zo_smoke|120|python -c 'import __graft_entry__ as g; g.smoke()'" \
+  "r5zo_bench|500|python bench.py > gpurun_out/r5zo_bench.json 2> gpurun_out/r5zo_bench.err" \
+  "r5zo_prof_c2|150|$RP -d gpurun_out/r5zo_prof_c2 -o c2 -- python bench.py --config C2 $BQ" \
+  "r5zo_prof_c3|150|$RP -d gpurun_out/r5zo_prof_c3 -o c3 -- python bench.py --config C3 $BQ" \
+  "r5zo_prof_c5|150|$RP -d gpurun_out/r5zo_prof_c5 -o c5 -- python bench.py --config C5 $BQ"
