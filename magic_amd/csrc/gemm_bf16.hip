@@ -738,7 +738,10 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
       if (s > 1 && (size_t)d.batch * s * d.M * d.N > max_ws) break;
       const double rounds = std::ceil(tiles * s / 256.0);
       double t = rounds * (np * std::ceil((double)kt / s) + fix) * t_kt;
-      if (s > 1) t += (double)d.batch * s * d.M * d.N * 8.0 / 4.5e12 + 4e-6;
+      // split-K: the slabs' write + read and the reduction launch (8 us fixed: C2's f32x hidden
+      // forward, 12288 x 500 x 501, ran 65.6 us at 192x256 split 2 against 61.0 us as one round
+      // of 192x128 tiles unsplit, where the model with 4 us preferred the split, r5zq)
+      if (s > 1) t += (double)d.batch * s * d.M * d.N * 8.0 / 4.5e12 + 8e-6;
       if (t < best * 0.97) { best = t; pl.split = s; pl.tn = w; pl.tm = tmr; }
     }
   }

@@ -833,8 +833,10 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
     const long long tm = (f.M + 255) / 256, tn = (f.N + 255) / 256, tiles = tm * tn;
     const long long n1 = (tiles / 256) * 256 / tm;  // n-tiles of the whole rounds
     c->f_split = false;
+    // (the rest at least 128 columns wide: a narrower one is no ring-kernel shape and would run on
+    // the 128x128 plane kernel, which the split's same-results argument does not cover)
     if (on && f.prec != GEMM_F32 && !f.valu && gemm_bf16_wide(f) && tiles > 256 && tiles % 256 != 0 &&
-        tiles % 256 <= 128 && n1 >= 1 && n1 < tn) {
+        tiles % 256 <= 128 && n1 >= 1 && n1 < tn && f.N - 256 * n1 >= 128) {
       const int c0 = (int)(256 * n1);
       GemmDesc a = f, b = f;
       a.N = c0;

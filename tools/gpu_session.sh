@@ -1,17 +1,15 @@
 #!/bin/bash
 # The current GPU session (overwritten per session; earlier sessions are in git history):
 #   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r5zo: verification of the tree after the decoder chain: full GPU suite, smoke, the default bench line (CPU baseline + PMC
-# traffic + configs block), per-config rocprofv3 kernel-trace runs (C2, C3, C5).
+# r5zr: the planner's split-K fixed cost 4 -> 8 us (C2's f32x hidden forward unsplit at 192x128):
+# plans of both libraries at C2 / C3 / C5, then the steps against the parent, alternating.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-export TMPDIR=/tmp
-PT="python -u -m pytest -q --maxfail=10 --timeout 120 --timeout-method thread -p no:cacheprovider"
-RP="rocprofv3 --kernel-trace --stats -f csv"
-BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 10 --warmup 3"
+BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 100"
+r() { echo "r5zr_$1|120|$3 python bench.py --config $2 $BQ > gpurun_out/r5zr_$1.json"; }
+H="MVAE_LIB=magic_amd/libmvae_head.so"
+p() { echo "r5zr_plan_$1_$2|120|$3 python bench.py --config $1 $BQ --steps 2 --create-opt plan_log=1 > gpurun_out/r5zr_plan_$1_$2.json"; }
 bash tools/gpu_steps.sh \
-  "r5zo_tests|400|$PT tests -m gpu" \
-  "r5zo_smoke|120|python -c 'import __graft_entry__ as g; g.smoke()'" \
-  "r5zo_bench|500|python bench.py > gpurun_out/r5zo_bench.json 2> gpurun_out/r5zo_bench.err" \
-  "r5zo_prof_c2|150|$RP -d gpurun_out/r5zo_prof_c2 -o c2 -- python bench.py --config C2 $BQ" \
-  "r5zo_prof_c3|150|$RP -d gpurun_out/r5zo_prof_c3 -o c3 -- python bench.py --config C3 $BQ" \
-  "r5zo_prof_c5|150|$RP -d gpurun_out/r5zo_prof_c5 -o c5 -- python bench.py --config C5 $BQ"
+  "$(p C2 h "$H")" "$(p C2 n)" "$(p C3 h "$H")" "$(p C3 n)" "$(p C5 h "$H")" "$(p C5 n)" \
+  "$(r c2_h1 C2 "$H")" "$(r c2_n1 C2)" "$(r c2_h2 C2 "$H")" "$(r c2_n2 C2)" "$(r c2_h3 C2 "$H")" "$(r c2_n3 C2)" \
+  "$(r c3_h1 C3 "$H")" "$(r c3_n1 C3)" "$(r c3_h2 C3 "$H")" "$(r c3_n2 C3)" \
+  "$(r c5_h1 C5 "$H")" "$(r c5_n1 C5)" "$(r c5_h2 C5 "$H")" "$(r c5_n2 C5)"
