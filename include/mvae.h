@@ -188,7 +188,12 @@ int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* cou
  * backward has written their gradients (beside the layer-0 weight gradient): only for callers
  * that neither read nor modify MVAE_BUF_GRADS between mvae_backward and mvae_adam (no
  * all-reduce): the caller's stream then joins the side stream in mvae_adam;
- * mvae_train_step uses it in the bf16 and f32x modes; "bce_split" (default 1) runs a BCE head whose
+ * mvae_train_step uses it in the bf16 and f32x modes; "early_chunks" (1, 2, 4, 8; default 2):
+ * with the early Adam and "wgrad0_chunks" 1, mvae_backward runs the layer-0 weight gradient in
+ * that many row chunks and updates each chunk's parameter rows but the last's on the side stream
+ * beside the next chunk's GEMM, i.e. already inside mvae_backward (so with early_adam the
+ * parameters, their Adam state and MVAE_BUF_GRADS are not to be read between mvae_backward and
+ * mvae_adam; 1: one GEMM, everything in mvae_adam); "bce_split" (default 1) runs a BCE head whose
  * 256x256 tiles leave a partial last round as the whole rounds plus 256x128 tiles for the rest
  * (the same results); "side_mask" (0-3, default 3): which weight gradients run on the side
  * stream -- bit 0 the decoder's, bit 1 the encoder's (a cleared bit: in order on the caller's

@@ -105,6 +105,12 @@ struct mvae_ctx {
   bool early_adam = false;   // option "early_adam": Adam of the parameters after the layer-0
                              // block runs on the side stream beside the layer-0 weight gradient
   bool early_fork = false;   // ... the side stream waits for the dgrad chain this step
+  // ... and, with the layer-0 weight gradient in R > 1 chunks, Adam of chunk k's rows ran on the
+  // side stream beside chunk k + 1's GEMM: mvae_adam's layer-0 launch starts here
+  size_t adam0_from = 0;
+  // the single-call backward with the early Adam runs the layer-0 weight gradient in this many
+  // chunks when "wgrad0_chunks" is 1 (option "early_chunks"; 1: one GEMM)
+  int early_chunks = 2;
   int side_mask = 3;         // option "side_mask": weight gradients on the side stream -- bit 0
                              // the decoder's, bit 1 the encoder's (else in order on the caller's)
   bool valu = true;          // skinny GEMMs on the fp32 VALU kernel (env MVAE_NO_VALU=1: off)
@@ -1307,6 +1313,21 @@ static int shadow_deint(mvae_ctx* ctx, hipStream_t st) {
   return MVAE_OK;
 }
 
+// Adam's arguments for this step (TF ApplyAdam: lr_t = lr * sqrt(1 - beta2_power) /
+// (1 - beta1_power), all fp32), the whole index range
+static AdamArgs adam_args(const mvae_ctx* c) {
+  AdamArgs a;
+  a.theta = c->theta; a.g1 = c->grads; a.g2 = c->grads + c->n_all;
+  a.m1 = c->adam; a.v1 = c->adam + c->n_all;
+  a.m2 = c->adam + 2 * c->n_all; a.v2 = c->adam + 2 * c->n_all + c->n_enc;
+  a.n_all = c->n_all; a.n_enc = c->n_enc;
+  a.b1 = c->cfg.beta1; a.b2 = c->cfg.beta2; a.eps = c->cfg.epsilon;
+  a.lr1 = (c->cfg.lr[0] * std::sqrt(1.f - c->b2p[0])) / (1.f - c->b1p[0]);
+  a.lr2 = (c->cfg.lr[1] * std::sqrt(1.f - c->b2p[1])) / (1.f - c->b1p[1]);
+  a.tp = planes_of(c, c->theta);
+  return a;
+}
+
 static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec) {
   auto c = ctx;
   int rc;
@@ -1327,6 +1348,18 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
   auto w0chunk = [&](int r) -> int {  // layer-0 weight gradient, chunk r of R
     const GemmDesc& d = R == 1 ? c->bwd_enc[n] : c->w0c[c->w0_chunks][r];
     return run(c, d, st, c->bwd_enc_r[n]);
+  };
+  // early Adam with R > 1 chunks: chunk k's rows (final in g1 and g2 after its GEMM) updated on the
+  // side stream beside chunk k + 1's GEMM, which reads no weights (elementwise: the same values)
+  auto chunk_adam = [&](int k) -> int {
+    if (!c->early_fork || !c->side || R == 1 || k >= R - 1 || c->enc[0].off != 0) return MVAE_OK;
+    AdamArgs a = adam_args(c);
+    a.i0 = c->adam0_from;
+    a.i1 = (size_t)c->w0m[c->w0_chunks][k + 1] * c->enc[0].ld;
+    if (int rc2 = stream_wait(c, st, c->side)) return rc2;
+    MV_CHECK(launch_adam(a, c->side));
+    c->adam0_from = a.i1;
+    return MVAE_OK;
   };
   auto tower = [&]() -> int {  // back through the conv tower (its gradients final after it)
     if (!c->conv) return MVAE_OK;
@@ -1404,14 +1437,17 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
     // mvae_backward_part all-reduces the gradients between the parts and mvae_adam, and the side
     // stream is not ordered after those collectives
     c->early_fork = false;
+    c->adam0_from = 0;
     if (c->early_adam && two && !join_dec) {
       if ((rc = fork())) return rc;
       c->early_fork = true;
     }
     if ((rc = w0chunk(0))) return rc;
+    if ((rc = chunk_adam(0))) return rc;
     if (R == 1 && (rc = tower())) return rc;
   } else if (part <= R) {
     if ((rc = w0chunk(part - 1))) return rc;
+    if ((rc = chunk_adam(part - 1))) return rc;
     if (part == R && (rc = tower())) return rc;
   } else if (!c->early_fork) {
     if ((rc = join())) return rc;
@@ -1437,10 +1473,16 @@ extern "C" int mvae_backward_part(mvae_ctx* ctx, int part, void* stream) {
 extern "C" int mvae_backward(mvae_ctx* ctx, void* stream) {
   if (!ctx) return MVAE_EINVAL;
   if (ctx->phase != 2) return fail(ctx, MVAE_ESTATE, "mvae_backward before mvae_metric");
-  int rc;
-  for (int part = 0; part < nparts(ctx); ++part)
-    if ((rc = backward_part(ctx, part, (hipStream_t)stream, false))) return rc;
-  return MVAE_OK;
+  // early Adam: the layer-0 weight gradient in early_chunks chunks, Adam of each chunk but the last
+  // beside the next chunk's GEMM (C2 -0.003, C3 -0.003, C5 -0.034 ms at 2 chunks, r5zw)
+  const int w0 = ctx->w0_chunks;
+  if (ctx->early_adam && ctx->use_side && ctx->side && w0 == 1 && ctx->early_chunks > 1 && !ctx->conv &&
+      ctx->enc[0].off == 0)
+    ctx->w0_chunks = ctx->early_chunks;
+  int rc = MVAE_OK;
+  for (int part = 0; part < nparts(ctx) && !rc; ++part) rc = backward_part(ctx, part, (hipStream_t)stream, false);
+  ctx->w0_chunks = w0;
+  return rc;
 }
 
 extern "C" int mvae_set_option(mvae_ctx* ctx, const char* name, int value) {
@@ -1469,6 +1511,13 @@ extern "C" int mvae_set_option(mvae_ctx* ctx, const char* name, int value) {
     // mvae_backward only; the per-part API (mvae_backward_part, the all-reduce path) ignores it
     if (ctx->phase == 4) return fail(ctx, MVAE_ESTATE, "early_adam cannot change mid-backward");
     ctx->early_adam = value != 0;
+    return MVAE_OK;
+  }
+  if (k == "early_chunks") {
+    if (value != 1 && value != 2 && value != 4 && value != 8)
+      return fail(ctx, MVAE_EINVAL, "early_chunks must be 1, 2, 4 or 8");
+    if (ctx->phase == 4) return fail(ctx, MVAE_ESTATE, "early_chunks cannot change mid-backward");
+    ctx->early_chunks = value;
     return MVAE_OK;
   }
   if (k == "wgrad0_chunks") {
@@ -1516,16 +1565,7 @@ extern "C" int mvae_adam(mvae_ctx* ctx, void* stream) {
   if (!ctx) return MVAE_EINVAL;
   if (ctx->phase != 3) return fail(ctx, MVAE_ESTATE, "mvae_adam before mvae_backward");
   auto c = ctx;
-  AdamArgs a;
-  a.theta = c->theta; a.g1 = c->grads; a.g2 = c->grads + c->n_all;
-  a.m1 = c->adam; a.v1 = c->adam + c->n_all;
-  a.m2 = c->adam + 2 * c->n_all; a.v2 = c->adam + 2 * c->n_all + c->n_enc;
-  a.n_all = c->n_all; a.n_enc = c->n_enc;
-  a.b1 = c->cfg.beta1; a.b2 = c->cfg.beta2; a.eps = c->cfg.epsilon;
-  // TF ApplyAdam: lr_t = lr * sqrt(1 - beta2_power) / (1 - beta1_power), all fp32
-  a.lr1 = (c->cfg.lr[0] * std::sqrt(1.f - c->b2p[0])) / (1.f - c->b1p[0]);
-  a.lr2 = (c->cfg.lr[1] * std::sqrt(1.f - c->b2p[1])) / (1.f - c->b1p[1]);
-  a.tp = planes_of(c, c->theta);
+  const AdamArgs a = adam_args(c);
   hipStream_t st = (hipStream_t)stream;
   if (c->early_fork && c->side) {
     // the blocks after layer 0 on the side stream (already past the dgrad chain), layer 0 and the
@@ -1534,7 +1574,9 @@ extern "C" int mvae_adam(mvae_ctx* ctx, void* stream) {
     const size_t l1 = c->nenc > 1 ? c->enc[1].off : c->head.off;
     AdamArgs a1 = a, a0 = a;
     a1.i0 = l1;
+    a0.i0 = c->adam0_from;  // (the layer-0 chunks before the last: updated in the backward)
     a0.i1 = l1;
+    c->adam0_from = 0;
     MV_CHECK(launch_adam(a1, c->side));
     {
       TIMED("adam");

@@ -311,19 +311,27 @@ def test_side_stream_schedule_is_bitwise_identical(prec):
 def test_early_adam_is_bitwise_identical(prec):
     """Option early_adam (Adam of the blocks after layer 0 on the side stream, beside the layer-0
     weight gradient) vs one Adam launch after the backward, and mvae_train_step (which uses it
-    in the plane modes): bitwise identical parameters after three steps."""
+    in the plane modes): bitwise identical parameters after three steps; and with the layer-0
+    weight gradient in two chunks (chunk 0's rows updated beside chunk 1's GEMM, the default of
+    the early Adam: option early_chunks) vs the same chunks with one Adam launch."""
     cfg = preset("8c", image_size=40, batch=768, precision=prec).replace(enc=(400, 300, 260))
     P = make_params(cfg)
     X, areas, eps = make_inputs(cfg, cfg.batch)
     x, a, e = to_dev(X), to_dev(areas), to_dev(eps)
-    outs = []
-    for mode in ("early", "late", "train_step"):
+    outs, outs2 = [], []
+    for mode in ("early", "late", "train_step", "early2", "late2", "train_step2"):
         eng = _engine(cfg)  # fresh Adam state per mode
         try:
-            eng.set_option("early_adam", 1 if mode == "early" else 0)
+            eng.set_option("early_adam", 1 if mode.startswith("early") else 0)
+            if mode == "train_step2":  # the default: two chunks under the early Adam
+                pass
+            elif mode.endswith("2"):  # layer-0 weight gradient in two chunks: chunk 0's Adam early
+                eng.set_option("wgrad0_chunks", 2)
+            else:  # one layer-0 GEMM, also with the early Adam (default: early_chunks = 2)
+                eng.set_option("early_chunks", 1)
             eng.load_params(P)
             for _ in range(3):
-                if mode == "train_step":
+                if mode.startswith("train_step"):
                     eng.train_step(x, a, e)
                 else:
                     eng.forward(x, e)
@@ -331,12 +339,13 @@ def test_early_adam_is_bitwise_identical(prec):
                     eng.backward()
                     eng.adam()
             torch.cuda.synchronize()
-            outs.append({k: v.cpu().numpy() for k, v in eng.params().items()})
+            (outs2 if mode.endswith("2") else outs).append({k: v.cpu().numpy() for k, v in eng.params().items()})
         finally:
             eng.close()
-    for o in outs[1:]:
-        for k in outs[0]:
-            np.testing.assert_array_equal(outs[0][k], o[k])
+    for group in (outs, outs2):
+        for o in group[1:]:
+            for k in group[0]:
+                np.testing.assert_array_equal(group[0][k], o[k])
 
 
 

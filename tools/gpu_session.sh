@@ -1,9 +1,15 @@
 #!/bin/bash
 # The current GPU session (overwritten per session; earlier sessions are in git history):
 #   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r5zu: C2's thin GEMMs (latent head, decoder layer 1) in the fp32-accurate forms: the f32x ring
-# kernel on any shape (v35 = prec 2 + variant 3, the step's thin_ring plan), native fp32 MFMA (v0),
-# the fp32 VALU kernel (v9), with their epilogues.
+# r5zx: option early_chunks (default 2): under the early Adam the single-call backward runs the
+# layer-0 weight gradient in 2 row chunks, chunk 0's Adam beside chunk 1's GEMM. Tests, then
+# C2 / C3 / C5 against the parent commit's library, alternating.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-GB="python tools/gemm_bench.py --config C2 --epilogues --variants 35,0,9 --rounds 5 --shapes head_fwd,head_bwd_d,head_bwd_w,dec_fwd_1,dec_bwd_w_1,dec_bwd_d_z"
-bash tools/gpu_steps.sh "r5zu|300|$GB"
+BQ="--no-cpu-baseline --pmc off --no-configs --no-h2d --no-pipeline --steps 100"
+r() { echo "r5zx_$1|120|$3 python bench.py --config $2 $BQ > gpurun_out/r5zx_$1.json"; }
+H="MVAE_LIB=magic_amd/libmvae_head.so"
+bash tools/gpu_steps.sh \
+  "r5zx_t|600|python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_r2.py tests/test_gpu_dp.py tests/test_gpu_r3.py tests/test_gpu_parity.py tests/test_gpu_golden.py" \
+  "$(r c2_h1 C2 "$H")" "$(r c2_n1 C2)" "$(r c2_h2 C2 "$H")" "$(r c2_n2 C2)" "$(r c2_h3 C2 "$H")" "$(r c2_n3 C2)" \
+  "$(r c3_h1 C3 "$H")" "$(r c3_n1 C3)" "$(r c3_h2 C3 "$H")" "$(r c3_n2 C3)" \
+  "$(r c5_h1 C5 "$H")" "$(r c5_n1 C5)" "$(r c5_h2 C5 "$H")" "$(r c5_n2 C5)"
