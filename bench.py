@@ -18,8 +18,10 @@ contract's fields the line carries:
                  mean HIP-event duration in the timed loop, against the dense MFMA peak of
                  the arithmetic it runs on; f32x (fp32-accurate bf16 plane split) adds
                  mfma_pipe_frac = plane-pair bf16 work / time / bf16 peak. traffic = HBM
-                 bytes per launch from rocprofv3 FETCH_SIZE / WRITE_SIZE passes run by this
-                 process (child runs, marker-bracketed region, MI355X_MICROARCH.md §HBM).
+                 bytes per step of that region (its launches: the layer-0 weight gradient runs
+                 as 2 row chunks under the early Adam) from rocprofv3 FETCH_SIZE / WRITE_SIZE
+                 passes run by this process (child runs, marker-bracketed, MI355X_MICROARCH.md
+                 §HBM); achieved and avg_ms are per step as well.
   loss_roofline  the HBM-bound kernels (de-interleave, sampler, latent head, metric, Adam)
                  and the BCE epilogue: algorithmic bytes per launch / time vs 8 TB/s.
   cpu_baseline   the CPU restatement (oracle, numpy fp32 + BLAS) on this host: the
@@ -267,8 +269,15 @@ def _region_ns(d, region_ids):
 N_SIMD = 1024  # 256 CUs x 4 SIMDs (MI355X)
 
 
-def pmc_traffic(args, names, regions_all, config=None, mfma=()):
-    """HBM bytes per launch of each region in `names`: two rocprofv3 child runs of this bench
+def launches_per_step(args, regions):
+    """Launches per step of each timed region (region pass: launch count / steps)."""
+    return {k: max(1, round(v[1] / args.region_steps)) for k, v in regions.items()}
+
+
+def pmc_traffic(args, names, regions_all, config=None, mfma=(), lps=None):
+    """HBM bytes per step of each region in `names` (the mean per bracketed launch x `lps[name]`,
+    the region's launches per step: 2 for the BCE head split and the chunked layer-0 weight
+    gradient): two rocprofv3 child runs of this bench
     (FETCH_SIZE and WRITE_SIZE cannot share a pass), markers around the regions; FETCH_SIZE x2
     (MI355X_MICROARCH.md: gfx950 reports half of a wide streaming read) and KB -> B. For the
     regions in `mfma`, a third pass (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE): the matrix-pipe
@@ -316,20 +325,23 @@ def pmc_traffic(args, names, regions_all, config=None, mfma=()):
             ns = _region_ns(d, list(ids.values()))
     out = {}
     for n, rid in ids.items():
+        k = (lps or {}).get(n, 1)
         f, w = res["FETCH_SIZE"].get(rid), res["WRITE_SIZE"].get(rid)
         if f is not None and w is not None:
-            out[n] = {"hbm_bytes": round(f * 1024 * 2 + w * 1024),
-                      "fetch_bytes": round(f * 1024 * 2), "write_bytes": round(w * 1024)}
+            out[n] = {"hbm_bytes": round(k * (f * 1024 * 2 + w * 1024)),
+                      "fetch_bytes": round(k * f * 1024 * 2), "write_bytes": round(k * w * 1024)}
+            if k != 1:
+                out[n]["launches_per_step"] = k
         busy, gui = res.get("SQ_VALU_MFMA_BUSY_CYCLES", {}).get(rid), res.get("GRBM_GUI_ACTIVE", {}).get(rid)
         if n in mfma and busy and gui:
             cyc = gui / 8.0
             e = out.setdefault(n, {})
             e["mfma_busy"] = round(busy / (N_SIMD * cyc), 4)
-            e["mfma_busy_cycles"] = round(busy)
-            e["kernel_cycles"] = round(cyc)
+            e["mfma_busy_cycles"] = round(k * busy)
+            e["kernel_cycles"] = round(k * cyc)
             if ns.get(rid):
                 e["clock_ghz"] = round(cyc / ns[rid], 3)
-                e["profiled_ms"] = round(ns[rid] / 1e6, 4)
+                e["profiled_ms"] = round(k * ns[rid] / 1e6, 4)
     return out, (f"rocprofv3 child passes of this bench ({config or args.config}), marker-bracketed: "
                  f"--pmc FETCH_SIZE / WRITE_SIZE" + (" / SQ_VALU_MFMA_BUSY_CYCLES + GRBM_GUI_ACTIVE" if mfma else "")
                  + f" ({root})")
@@ -939,7 +951,8 @@ def main():
                 if rf and world == 1 and args.pmc == "auto" and not args.dry_run:
                     mf = [m["dom"]] + [k for k in PMC_REGIONS_MFMA if k in m["regions"] and k != m["dom"]]
                     want = mf + [k for k in PMC_REGIONS_BW if k in m["regions"]]
-                    tr, how = pmc_traffic(args, want, names_c, config=cid, mfma=tuple(mf))
+                    tr, how = pmc_traffic(args, want, names_c, config=cid, mfma=tuple(mf),
+                                          lps=launches_per_step(args, m["regions"]))
                     rf["traffic_method"] = how
                     if tr and m["dom"] in tr:
                         rf["traffic"] = tr[m["dom"]].get("hbm_bytes")
@@ -974,7 +987,7 @@ def main():
             names = eng.timing_names()
             mf = [head["dom"]] + [k for k in PMC_REGIONS_MFMA if k in head["regions"] and k != head["dom"]]
             want = mf + [k for k in PMC_REGIONS_BW if k in head["regions"]]
-            tr, how = pmc_traffic(args, want, names, mfma=tuple(mf))
+            tr, how = pmc_traffic(args, want, names, mfma=tuple(mf), lps=launches_per_step(args, head["regions"]))
             roofline["traffic_method"] = how
             if tr:
                 if head["dom"] in tr:
