@@ -269,15 +269,9 @@ def _region_ns(d, region_ids):
 N_SIMD = 1024  # 256 CUs x 4 SIMDs (MI355X)
 
 
-def launches_per_step(args, regions):
-    """Launches per step of each timed region (region pass: launch count / steps)."""
-    return {k: max(1, round(v[1] / args.region_steps)) for k, v in regions.items()}
-
-
-def pmc_traffic(args, names, regions_all, config=None, mfma=(), lps=None):
-    """HBM bytes per step of each region in `names` (the mean per bracketed launch x `lps[name]`,
-    the region's launches per step: 2 for the BCE head split and the chunked layer-0 weight
-    gradient): two rocprofv3 child runs of this bench
+def pmc_traffic(args, names, regions_all, config=None, mfma=()):
+    """HBM bytes per step of each region in `names` (the mean per bracketed launch x the region's
+    launches per child step: 2 for the BCE head split and the chunked layer-0 weight gradient): two rocprofv3 child runs of this bench
     (FETCH_SIZE and WRITE_SIZE cannot share a pass), markers around the regions; FETCH_SIZE x2
     (MI355X_MICROARCH.md: gfx950 reports half of a wide streaming read) and KB -> B. For the
     regions in `mfma`, a third pass (SQ_VALU_MFMA_BUSY_CYCLES, GRBM_GUI_ACTIVE): the matrix-pipe
@@ -291,6 +285,7 @@ def pmc_traffic(args, names, regions_all, config=None, mfma=(), lps=None):
     base = os.path.join(HERE, "gpurun_out") if os.path.isdir(os.path.join(HERE, "gpurun_out")) \
         else tempfile.gettempdir()
     root = tempfile.mkdtemp(prefix="bench_pmc_", dir=base)
+    child_steps = 3  # every child step runs the markers
     child = [sys.executable, os.path.abspath(__file__), "--pmc-child", ",".join(str(r) for r in ids.values()),
              "--config", config or args.config, "--steps", "2", "--warmup", "1"]
     if args.batch and config is None:
@@ -302,7 +297,7 @@ def pmc_traffic(args, names, regions_all, config=None, mfma=(), lps=None):
     passes = [("fetch", ["FETCH_SIZE"]), ("write", ["WRITE_SIZE"])]
     if mfma:
         passes.append(("mfma", ["SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"]))
-    res, ns = {}, {}
+    res, ns, nl = {}, {}, {}
     for tag, counters in passes:
         d = os.path.join(root, tag)
         cmd = [exe, "--pmc", *counters, "--kernel-trace", "--output-format", "csv", "-d", d, "-o", "run",
@@ -321,11 +316,13 @@ def pmc_traffic(args, names, regions_all, config=None, mfma=(), lps=None):
             return None, f"{tag} pass rc={rc} (log {root})"
         for c in counters:
             res[c] = _region_counter(d, c, list(ids.values()))
+        if tag == "fetch":
+            nl = {rid: len(g) for rid, g in _region_dispatches(d, list(ids.values())).items()}
         if tag == "mfma":
             ns = _region_ns(d, list(ids.values()))
     out = {}
     for n, rid in ids.items():
-        k = (lps or {}).get(n, 1)
+        k = max(1, round(nl.get(rid, child_steps) / child_steps))
         f, w = res["FETCH_SIZE"].get(rid), res["WRITE_SIZE"].get(rid)
         if f is not None and w is not None:
             out[n] = {"hbm_bytes": round(k * (f * 1024 * 2 + w * 1024)),
@@ -951,8 +948,7 @@ def main():
                 if rf and world == 1 and args.pmc == "auto" and not args.dry_run:
                     mf = [m["dom"]] + [k for k in PMC_REGIONS_MFMA if k in m["regions"] and k != m["dom"]]
                     want = mf + [k for k in PMC_REGIONS_BW if k in m["regions"]]
-                    tr, how = pmc_traffic(args, want, names_c, config=cid, mfma=tuple(mf),
-                                          lps=launches_per_step(args, m["regions"]))
+                    tr, how = pmc_traffic(args, want, names_c, config=cid, mfma=tuple(mf))
                     rf["traffic_method"] = how
                     if tr and m["dom"] in tr:
                         rf["traffic"] = tr[m["dom"]].get("hbm_bytes")
@@ -987,7 +983,7 @@ def main():
             names = eng.timing_names()
             mf = [head["dom"]] + [k for k in PMC_REGIONS_MFMA if k in head["regions"] and k != head["dom"]]
             want = mf + [k for k in PMC_REGIONS_BW if k in head["regions"]]
-            tr, how = pmc_traffic(args, want, names, mfma=tuple(mf), lps=launches_per_step(args, head["regions"]))
+            tr, how = pmc_traffic(args, want, names, mfma=tuple(mf))
             roofline["traffic_method"] = how
             if tr:
                 if head["dom"] in tr:
