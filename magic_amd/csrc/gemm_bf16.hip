@@ -711,7 +711,9 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
   // the eight-phase kernel addresses an operand plane by 32-bit per-lane element offsets
   const long long ea = (long long)(d.at ? d.K : d.M) * d.lda, eb = (long long)(d.bt ? d.N : d.K) * d.ldb;
   const bool e8_fits = ea < (1LL << 32) && eb < (1LL << 32);
-  const bool allow_e8 = e8_fits && (force_e8 || (d.variant == 0 && e8_rule));
+  // A as bits (a 0/1 operand): the eight-phase kernel, whose bits path reads it (its plane path
+  // runs the rare batch with another pixel value)
+  const bool allow_e8 = e8_fits && (force_e8 || (d.variant == 0 && (e8_rule || d.Abits)));
   double best = 1e30;
   WidePlan pl;
   for (int cand = 0; cand < 5; ++cand) {
@@ -720,6 +722,7 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
     const int w = cand == 0 || cand == 3 ? 256 : cand == 1 || cand == 4 ? 128 : TN_E8;
     const int tmr = cand >= 3 ? 192 : 256;
     if (e8 ? !allow_e8 : allow_e8 || (force_e8 && e8_fits)) continue;
+    if (!e8 && d.Abits && e8_fits && d.variant == 0) continue;
     if (cand >= 3 && !t192) continue;
     if ((d.tm == 192 && t192 && cand != 3 && cand != 4) || (d.tm == 256 && cand >= 3)) continue;
     if (d.variant == 11 && w != 128) continue;
@@ -767,6 +770,7 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   p.dyn = d.dynA;
   p.diag = d.diag;
   p.stamps = d.stamps;
+  p.abits = d.Abits; p.abits_kts = d.abits_kts; p.abits_sb = d.abits_sb; p.anb = d.anb;
   // tile order: bands of 8 m-tiles walked n by n when a row has >= 8 n-tiles, so the 32 tiles
   // an XCD holds at once share 8 A and 4 B tiles in its L2 (C5 latent-head forward
   // 24576 x 4000 x 501: 0.177 -> 0.161 ms; neutral on the BCE head and the other shapes,
@@ -785,6 +789,7 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
     }
   p.npairs = n;
   p.npairs0 = d.nB < T ? d.nB : T;  // pairs with i == 0
+  p.npairs_a0 = p.npairs0;
   if (!p.dyn) p.npairs0 = n;
   p.pab = 0;
   for (int i = 0; i < n; ++i) p.pab |= (p.pa[i] | p.pb[i] << 2) << (4 * i);

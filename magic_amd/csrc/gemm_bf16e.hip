@@ -156,11 +156,48 @@ __device__ __forceinline__ void bar() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// ---- the bits path (BitMat A, mvae_internal.h): a k-tile's A image is its 2 KB block, copied by
+// one 256-B global_load_lds_dword per wave into one of two bits buffers at LDS 0 / 2048 (the A
+// half-image area is otherwise unused); each wave reads its two 64-row quarters (8 B per lane
+// each) with ds_read_b64 and expands them in registers into its 8 + 8 A fragments: 1.0 / 0.0
+// bf16 pairs, two VALU operations per dword (the fragments the plane path reads from LDS).
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+template <int OFF>
+__device__ __forceinline__ u32x2 rd_b64(unsigned a) {
+  u32x2 v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+  return v;
+}
+// fragments (2 j + h, kh) of one quarter's word j: element pair d = bits (p, p + 16) of w >> 8 h,
+// p = 4 kh + d, as bf16 pair (1.0 | 0.0) = that masked word times 0x3F80 >> p (v_mul_u32_u24)
+__device__ __forceinline__ bf16x8 bits_frag(unsigned s, int kh) {
+  unsigned d[4];
+#pragma unroll
+  for (int dd = 0; dd < 4; ++dd) {
+    const int p = 4 * kh + dd;
+    d[dd] = (unsigned)__umul24(s & (0x10001u << p), 0x3F80u >> p);
+  }
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  return __builtin_bit_cast(bf16x8, u32x4{d[0], d[1], d[2], d[3]});
+}
+__device__ __forceinline__ void bits_expand(u32x2 w, bf16x8 (&fa)[8]) {
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const unsigned wj = j ? w.y : w.x;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const unsigned s = h ? wj >> 8 : wj;
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) fa[2 * (2 * j + h) + kh] = bits_frag(s, kh);
+    }
+  }
+}
+
 // main-loop state of one workgroup (registers once inlined). ST: stamped diagnostics build --
 // per wave the k-loop's shader-clock cycles and, with diag 16, each of a k-tile's 8
 // barrier-delimited slots summed over the k-loop (mvae_bench_gemm with MVAE_STAMPS=2; never in
-// the step)
-template <bool AT, bool BT, bool ST = false>
+// the step). BITS: A from a BitMat (the plane path's A images, reads and DMA are not used)
+template <bool AT, bool BT, bool ST = false, bool BITS = false>
 struct E8 {
   static constexpr bool KA = !AT, KB = BT;  // operand images k-contiguous?
   HLoad<KA> la;
@@ -178,6 +215,25 @@ struct E8 {
   int wave;
   unsigned long long st_last, st_acc[ST ? 8 : 1];
   bool st_slots;  // stamped builds, diag 16: per-slot stamps (each waits lgkmcnt(0): intrusive)
+  // BITS: this tile's strip (its first k-tile's block at Ab + 512 * (ks / 64)); LDS byte address
+  // of this wave's quarter-0 words in bits buffer 0 (quarter 1: + 1024, buffer 1: + 2048); the
+  // current k-tile's words of quarters 0 (A-sub 0) and 1 (A-sub 1)
+  const unsigned* Ab;
+  unsigned bA;
+  u32x2 wb0, wb1;
+
+  // BITS: the 2 KB block of k-tile kt into bits buffer Bf, 256 B per wave
+  template <int Bf>
+  __device__ __forceinline__ void issue_bits(const Tile& t, int kt) {
+    typedef __attribute__((address_space(3))) void* lds_ptr;
+    const unsigned* src = Ab + (size_t)(t.ks / EBK + kt) * BITMAT_BLOCK_WORDS + wave * 64 + (threadIdx.x & 63);
+    __builtin_amdgcn_global_load_lds(src, (lds_ptr)(reinterpret_cast<char*>(smem) + Bf * 2048 + wave * 256), 4, 0, 0);
+  }
+  template <int Bf>
+  __device__ __forceinline__ void rd_bits() {
+    wb0 = rd_b64<Bf * 2048>(bA);
+    wb1 = rd_b64<Bf * 2048 + 1024>(bA);
+  }
 
   template <int K>
   __device__ __forceinline__ void sbar() {
@@ -269,12 +325,23 @@ struct E8 {
     // p1 (0,0)
     if (rdf) rd_b<0, Bf>(fb0);
     __builtin_amdgcn_sched_barrier(0);
-    if (rdf) rd_a<0, Bf>(fa0);
-    if (h1 && !ka1) issue_a<1, Bn>(pp, t, kt1, pr1);
-    // the B-sub 0 reads (issued first) retired: B0 is restaged in p2
-    // (the A-sub 0 reads: 8 ds_read_b128, or 16 transposing reads -- the count saturates at 15)
-    if constexpr (KA) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-    else asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+    if constexpr (BITS) {
+      // both quarters' words (the buffer is next restaged in tile it+1's p1); the whole block of
+      // it+1 into the other buffer, whose last reads were tile it-1's p1; quarter 0 expanded once
+      // every read retired (B-sub 0's as well: B0 is restaged in p2)
+      rd_bits<Bf>();
+      if (h1 && !ka1) issue_bits<Bn>(t, kt1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      bits_expand(wb0, fa0);
+    } else {
+      if (rdf) rd_a<0, Bf>(fa0);
+      if (h1 && !ka1) issue_a<1, Bn>(pp, t, kt1, pr1);
+      // the B-sub 0 reads (issued first) retired: B0 is restaged in p2
+      // (the A-sub 0 reads: 8 ds_read_b128, or 16 transposing reads -- the count saturates at 15)
+      if constexpr (KA) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(15)" ::: "memory");
+    }
     sbar<0>();
     mfma_q<0, 0>(fa0, fb0);
     sbar<1>();
@@ -285,35 +352,38 @@ struct E8 {
     mfma_q<0, 1>(fa0, fb1);
     sbar<3>();
     // p3 (1,1)
-    if (rdf) rd_a<1, Bf>(fa1);
-    if (ia2) issue_a<0, Bf>(pp, t, kt2, pr2);
+    if constexpr (BITS) {
+      bits_expand(wb1, fa1);
+    } else {
+      if (rdf) rd_a<1, Bf>(fa1);
+      if (ia2) issue_a<0, Bf>(pp, t, kt2, pr2);
+    }
     sbar<4>();
     mfma_q<1, 1>(fa1, fb1);
     sbar<5>();
     // p4 (1,0): k-tile it+1 landed -- what stays in flight is the halves of it+2 issued in this
-    // tile (2 DMA instructions each)
+    // tile (2 DMA instructions each; the bits path's block of it+1 went out in p1, before them)
     if (ib2) issue_b<1, Bf>(pp, t, kt2, pr2);
-    if (ib2 && ia2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else if (ib2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else if (ia2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (BITS) {
+      if (ib2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (ib2 && ia2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (ib2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (ia2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     sbar<6>();
     mfma_q<1, 0>(fa1, fb0);
     sbar<7>();
   }
 };
 
-template <bool AT, bool BT, int EPI, bool TE, bool ST = false>
-__global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
+// One workgroup's tile: the k-loop and the epilogue. BITS: A from the BitMat pp.abits (its AT
+// is then immaterial: the bits path has one A layout)
+template <bool AT, bool BT, int EPI, bool TE, bool ST, bool BITS>
+__device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
   const Params& p = pp.g;
-  if (epi_skip<EPI>(p.epi)) return;
-  // [A0 b0 | A0 b1 | A1 b0 | A1 b1 | B0 b0 | B0 b1 | B1 b0 | B1 b1]; the row-major epilogue's two
-  // 64-row bands and the BCE row partials reuse it after the k-loop (one __shared__ array: a
-  // second one can make hipcc wait vmcnt(0) before the loop's LDS reads)
-  constexpr int RING = 8 * EH;
-  constexpr int EPIL = 2 * (2 * 64 * 256 + 64 * 4 * 32);
-  __shared__ __attribute__((aligned(1024))) short smem[RING > EPIL ? RING : EPIL];
-
   unsigned long long st_k0 = 0, st_k2 = 0;  // stamped builds: kernel start, k-loop end (realtime)
   if constexpr (ST) st_k0 = __builtin_amdgcn_s_memrealtime();
   const int tid = threadIdx.x;
@@ -321,14 +391,18 @@ __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
   const int wm = wave >> 2, wn = wave & 3;
   const Tile t = tile_of_t<256, 256>(p, true);
 
-  using S = E8<AT, BT, ST>;
+  using S = E8<AT, BT, ST, BITS>;
   S s;
   s.A = pp.A + t.bi * p.sA;
   s.Bm = pp.B + t.bi * p.sB;
   s.smem = smem;
   s.wave = __builtin_amdgcn_readfirstlane(wave);
   if constexpr (ST) s.st_slots = (pp.diag & 16) != 0;
-  s.la.init(p.lda, t.m0, p.M, wave, lane);
+  if constexpr (BITS) {
+    s.Ab = pp.abits + (size_t)t.bi * pp.abits_sb + (size_t)(t.m0 / 256) * pp.abits_kts * BITMAT_BLOCK_WORDS;
+  } else {
+    s.la.init(p.lda, t.m0, p.M, wave, lane);
+  }
   s.lb.init(p.ldb, t.n0, p.N, wave, lane);
 #pragma unroll
   for (int b = 0; b < 4; ++b)
@@ -339,7 +413,9 @@ __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) s.acc[b][i][j][k] = f32x4{0.f, 0.f, 0.f, 0.f};
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
-  if constexpr (S::KA) {
+  if constexpr (BITS) {
+    s.bA = lds0 + (unsigned)(wm * 512 + lane * 8);  // quarter (0, wm): rows 64 wm .. of half 0
+  } else if constexpr (S::KA) {
     s.aA[0] = lds0 + frag_addr<true>(64 * wm, lane);
   } else {
 #pragma unroll
@@ -352,7 +428,8 @@ __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
     for (int nb = 0; nb < 2; ++nb) s.aB[nb] = lds0 + 4 * EHB + frag_addr<false>(32 * wn + 16 * nb, lane);
   }
 
-  const int np = (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
+  // (bits: A is exact, its residual planes zero -- the pairs with A plane 0)
+  const int np = BITS ? pp.npairs_a0 : (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
   const int nkt = t.ks < t.ke ? (t.ke - t.ks + EBK - 1) / EBK : 0;
   const int total = np * nkt;
   // waves 4-7 (the second wave of every SIMD), as a scalar condition: s_barrier ignores EXEC
@@ -384,19 +461,33 @@ __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
     set(c0);
     c1 = c0; adv(c1);
     c2 = c1; adv(c2);
-    // prologue: A0 B0 B1 A1 of k-tile 0, then B0 A0 B1 of k-tile 1 (its A1: tile 0's p1)
-    s.template issue_a<0, 0>(pp, t, 0, 0);
-    s.template issue_b<0, 0>(pp, t, 0, 0);
-    s.template issue_b<1, 0>(pp, t, 0, 0);
-    s.template issue_a<1, 0>(pp, t, 0, 0);
+    // prologue: A0 B0 B1 A1 of k-tile 0, then B0 A0 B1 of k-tile 1 (its A1: tile 0's p1); the bits
+    // path: k-tile 0's block, B0 B1, then k-tile 1's B0 B1 (its block: tile 0's p1)
     int kt1 = c1.kt, pr1 = c1.pr, kt2 = c2.kt, pr2 = c2.pr;
-    if (total > 1) {
-      s.template issue_b<0, 1>(pp, t, kt1, pr1);
-      s.template issue_a<0, 1>(pp, t, kt1, pr1);
-      s.template issue_b<1, 1>(pp, t, kt1, pr1);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    if constexpr (BITS) {
+      s.template issue_bits<0>(t, 0);
+      s.template issue_b<0, 0>(pp, t, 0, 0);
+      s.template issue_b<1, 0>(pp, t, 0, 0);
+      if (total > 1) {
+        s.template issue_b<0, 1>(pp, t, kt1, pr1);
+        s.template issue_b<1, 1>(pp, t, kt1, pr1);
+        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      s.template issue_a<0, 0>(pp, t, 0, 0);
+      s.template issue_b<0, 0>(pp, t, 0, 0);
+      s.template issue_b<1, 0>(pp, t, 0, 0);
+      s.template issue_a<1, 0>(pp, t, 0, 0);
+      if (total > 1) {
+        s.template issue_b<0, 1>(pp, t, kt1, pr1);
+        s.template issue_a<0, 1>(pp, t, kt1, pr1);
+        s.template issue_b<1, 1>(pp, t, kt1, pr1);
+        asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
     bar();
     if (lag) bar();
@@ -472,6 +563,30 @@ __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
   }
 }
 
+// the bits path is compiled where the step runs it: the layer-0 forward (ACT, or split-K slabs)
+// and weight gradient (slabs or output), B row-contiguous
+template <bool BT, int EPI, bool ST>
+constexpr bool has_bits = !BT && !ST && (EPI == EPI_STORE || EPI == EPI_ACT);
+
+template <bool AT, bool BT, int EPI, bool TE, bool ST = false>
+__global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
+  if (epi_skip<EPI>(pp.g.epi)) return;
+  // [A0 b0 | A0 b1 | A1 b0 | A1 b1 | B0 b0 | B0 b1 | B1 b0 | B1 b1]; the row-major epilogue's two
+  // 64-row bands and the BCE row partials reuse it after the k-loop (one __shared__ array: a
+  // second one can make hipcc wait vmcnt(0) before the loop's LDS reads)
+  constexpr int RING = 8 * EH;
+  constexpr int EPIL = 2 * (2 * 64 * 256 + 64 * 4 * 32);
+  __shared__ __attribute__((aligned(1024))) short smem[RING > EPIL ? RING : EPIL];
+  // a 0/1 batch (the de-interleave's not-binary word, a uniform branch): A from its bits
+  if constexpr (has_bits<BT, EPI, ST>) {
+    if (pp.abits && (!pp.anb || *pp.anb == 0)) {
+      e8_tile<false, BT, EPI, TE, ST, true>(pp, smem);
+      return;
+    }
+  }
+  e8_tile<AT, BT, EPI, TE, ST, false>(pp, smem);
+}
+
 template <bool AT, bool BT, int EPI, bool TE>
 hipError_t launch_e(const PParams& p, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
@@ -498,7 +613,41 @@ hipError_t launch_e_t(const PParams& p, bool at, bool bt, bool te, hipStream_t s
   return te ? launch_e_l<EPI, true>(p, at, bt, st) : launch_e_l<EPI, false>(p, at, bt, st);
 }
 
+// (tests / diagnostics) one BitMat word per thread from a bf16 plane of 0/1 values
+__global__ void bits_from_plane_kernel(const unsigned short* __restrict__ plane, int ld, int trans, int M,
+                                       int K, unsigned* __restrict__ out, int kts, size_t nwords,
+                                       int* __restrict__ nb) {
+  const size_t w = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= nwords) return;
+  const size_t blk = w / BITMAT_BLOCK_WORDS;
+  const int r = (int)(w % BITMAT_BLOCK_WORDS);
+  const int mt = (int)(blk / kts), kt = (int)(blk % kts);
+  const int j = r & 1, lane = (r >> 1) & 63, q = r >> 7;  // q = 2 s + wm
+  unsigned word = 0;
+  bool bad = false;
+  for (int b = 0; b < 32; ++b) {
+    const int h = (b >> 3) & 1, kh = (b >> 2) & 1, el = ((b & 3) << 1) | (b >> 4);
+    const int row = mt * 256 + 64 * q + 16 * (2 * j + h) + (lane & 15);
+    const int k = kt * 64 + 32 * kh + 8 * (lane >> 4) + el;
+    if (row >= M || k >= K) continue;
+    const unsigned short v = trans ? plane[(size_t)k * ld + row] : plane[(size_t)row * ld + k];
+    if (v == 0x3F80u) word |= 1u << b;
+    else if (v != 0) bad = true;
+  }
+  out[w] = word;
+  if (bad && nb) atomicOr(nb, 1);
+}
+
 }  // namespace
+
+hipError_t launch_bits_from_plane(const unsigned short* plane, int ld, bool trans, int M, int K,
+                                  unsigned* out, int kts, int* nb, hipStream_t st) {
+  if (M <= 0 || K <= 0 || kts < bitmat_kts(K)) return hipErrorInvalidValue;
+  const size_t n = (size_t)((M + 255) / 256) * kts * BITMAT_BLOCK_WORDS;
+  hipLaunchKernelGGL(bits_from_plane_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, plane, ld,
+                     trans ? 1 : 0, M, K, out, kts, n, nb);
+  return hipGetLastError();
+}
 
 // the eight-phase kernel for a planned 256 x 256 tile (PParams::g.tn == TN_E8): te = the row-major
 // LDS epilogue with 16-B global accesses, else element-wise

@@ -44,6 +44,13 @@ struct PParams {
                                     // again when its buffer already holds it (gemm_bf16e.hip)
   unsigned long long* stamps;       // stamped diagnostics builds (ST): 8 slots per workgroup
                                     // {start, prologue landed, k-loop done, end, stores issued}
+  // eight-phase kernel: A as a BitMat (mvae_internal.h) instead of its planes while *anb == 0 --
+  // strips of kts blocks per 256 rows, batch stride sb words (GemmDesc::Abits)
+  const unsigned* abits = nullptr;
+  int abits_kts = 0;
+  long long abits_sb = 0;
+  const int* anb = nullptr;
+  int npairs_a0 = 1;                // the leading pairs with A plane 0 (the bits path's pairs)
 };
 
 // tanh as an odd [13/6] rational in x on [-7.905, 7.905] (clamped beyond, where tanh rounds to
@@ -215,6 +222,9 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
   constexpr bool BCE = EPI == EPI_BCE || EPI == EPI_BCEB;
   constexpr bool READS = is_dact<EPI> || BCE;
   const bool x16 = bce_x16<EPI>(e);
+  // a 0/1 batch whose target the de-interleave wrote as bits (with the pixel operand as bits it
+  // writes no bf16 plane): one bit per element
+  const bool tbits = EPI == EPI_BCEB && e.xnb && *e.xnb == 0 && e.xbits;
   const float* __restrict__ src = is_dact<EPI> ? e.aux : e.x;
   const int lds_ = is_dact<EPI> ? e.ld_aux : e.ldx;
   // not unrolled: the block's accumulators are acc[0], rotated down after each block (one copy
@@ -232,7 +242,8 @@ __device__ __forceinline__ void epilogue_g(const Params& p, const Tile& t, f32x1
         for (int ni = 0; ni < NI; ++ni) {
           int col = cbase + ni * 32;
           col = col < p.N ? col : p.N - 1;
-          if (EPI == EPI_BCEB && x16) sv[r][ni] = bf16_bits_to_f32(e.xp[(size_t)sr * lds_ + col]);
+          if (EPI == EPI_BCEB && tbits) sv[r][ni] = (float)((e.xbits[(size_t)sr * e.ldbits + (col >> 3)] >> (col & 7)) & 1);
+          else if (EPI == EPI_BCEB && x16) sv[r][ni] = bf16_bits_to_f32(e.xp[(size_t)sr * lds_ + col]);
           else if constexpr (is_dact<EPI>)
             sv[r][ni] = e.auxp ? bf16_bits_to_f32(e.auxp[(size_t)sr * lds_ + col]) : src[(size_t)sr * lds_ + col];
           else sv[r][ni] = src[(size_t)sr * lds_ + col];

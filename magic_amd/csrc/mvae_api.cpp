@@ -125,6 +125,13 @@ struct mvae_ctx {
   int x32dyn = 0;        // ... written only when *dyn != 0 (the BCE target, else read as bf16)
   unsigned char* xbits = nullptr;  // the BCE target (lock block) as bits (GemmEpi::xbits)
   int ldbits = 0;
+  // the layer-0 pixel operand of a 0/1 batch as bits (create option bits, default on where it
+  // applies): BitMats of the forward (3B x (D + 1)) and the weight gradient ((D + 1) x 3B), written
+  // by the de-interleave instead of the bf16 plane, read by the eight-phase kernel's bits path
+  bool bits_on = false;
+  unsigned* xbf = nullptr;
+  unsigned* xbw = nullptr;
+  int kts_f = 0, kts_w = 0;
   // schedule (each GEMM tagged with its timing region)
   std::vector<GemmDesc> fwd_enc;  // encoder layers + head
   // the hidden layers fwd_enc[1 .. nenc-1] as one launch (enc_chain.hip; create option enc_chain)
@@ -441,6 +448,8 @@ struct CreateOpts {
   int enc_chain_rows = 0;  // ... its rows per workgroup forced (16..96, multiple of 16; 0 auto)
   int diag_chain = 0;      // ... its timing ablations (ChainArgs::diag; results meaningless)
   int dec_chain = 1;    // bf16 mode: the decoder's two hidden layers in one launch (0: one GEMM each)
+  int bits = 1;         // the layer-0 pixel operand of a 0/1 batch as bits (BitMat): 1 in bf16 mode,
+                        // 2 in the f32x mode too, 0 never
   int conv2_nw = 8, conv2_tpb = 1, conv2_fpw = 2, conv2_wg = 8, conv2_half = 1, conv2_nchunk = 0;
 };
 
@@ -473,6 +482,7 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "enc_chain" && in(0, 1)) o->enc_chain = (int)v;
     else if (k == "diag_chain" && in(0, 7)) o->diag_chain = (int)v;
     else if (k == "dec_chain" && in(0, 1)) o->dec_chain = (int)v;
+    else if (k == "bits" && in(0, 2)) o->bits = (int)v;
     else if (k == "enc_chain_rows" && (v == 0 || (in(16, 96) && v % 16 == 0))) o->enc_chain_rows = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
     else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
@@ -812,6 +822,28 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
         mvae_destroy(c);
         return MVAE_EINVAL;
       }
+  {  // the pixel operand as bits: both layer-0 GEMMs on the bf16-plane kernels, the target bits
+     // written (D % 8 == 0), whole 64-row blocks, no fp32 pixel rows read
+    GemmDesc& f0 = c->fwd_enc[0];
+    GemmDesc& w0 = c->bwd_enc[c->nenc];
+    auto planek = [](const GemmDesc& d) { return d.prec != GEMM_F32 && !d.valu && gemm_bf16_wide(d); };
+    // (bf16 mode: in f32x the bits path expands A once per plane pair and measured slower, r6b)
+    if (opt.bits && (c->np == 1 || (opt.bits == 2 && c->np)) && !c->conv && c->xbits && c->B % 64 == 0 && c->x32mask == 0 && planek(f0) &&
+        planek(w0) && f0.A == c->xs && w0.A == c->xs) {
+      c->kts_f = bitmat_kts(c->D + 1);
+      c->kts_w = bitmat_kts(3 * c->B);
+      float* q = nullptr;
+      ALLOC(q, bitmat_words(3 * c->B, c->D + 1));
+      c->xbf = reinterpret_cast<unsigned*>(q);
+      ALLOC(q, bitmat_words(c->D + 1, 3 * c->B));
+      c->xbw = reinterpret_cast<unsigned*>(q);
+      f0.Abits = c->xbf; f0.abits_kts = c->kts_f; f0.anb = c->dyn + 2;
+      // the weight gradient's batch 2 (g2) reads stacked rows B .. 3B: k-tiles from B / 64
+      w0.Abits = c->xbw; w0.abits_kts = c->kts_w; w0.anb = c->dyn + 2;
+      w0.abits_sb = (long long)(c->B / 64) * BITMAT_BLOCK_WORDS;
+      c->bits_on = true;
+    }
+  }
   {  // layer-0 weight-gradient row chunks (see w0c): the wired GEMM re-pointed at row ranges
     const GemmDesc& w = c->bwd_enc[c->nenc];
     for (int R : {2, 4, 8}) {
@@ -823,6 +855,7 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
         d.A = w.A + m0;                  // A stored [K][M] (at): the chunk's columns
         if (d.Ap) d.Ap = w.Ap + m0;
         d.C = w.C + (size_t)m0 * w.ldc;  // output rows
+        if (d.Abits) d.Abits = w.Abits + (size_t)(m0 / 256) * w.abits_kts * BITMAT_BLOCK_WORDS;
         c->w0c[R].push_back(d);
         c->w0m[R].push_back(m0);
       }
@@ -1121,11 +1154,13 @@ static int run(mvae_ctx* ctx, const GemmDesc& d, hipStream_t st, int r = -1) {
   const bool sd = st == ctx->side && ctx->side;
   float* ws = sd ? ctx->ws_side : ctx->ws;
   // descriptors name the pixel flag by its first slot; the last de-interleave raised dyn_cur
-  if (ctx->dyn_cur && ctx->dyn_cur != ctx->dyn && (d.dynA == ctx->dyn || d.epi.xdyn == ctx->dyn)) {
+  if (ctx->dyn_cur && ctx->dyn_cur != ctx->dyn &&
+      (d.dynA == ctx->dyn || d.epi.xdyn == ctx->dyn || d.anb == ctx->dyn + 2)) {
     GemmDesc dd = d;
     if (dd.dynA == ctx->dyn) dd.dynA = ctx->dyn_cur;
     if (dd.epi.xdyn == ctx->dyn) dd.epi.xdyn = ctx->dyn_cur;
     if (dd.epi.xnb == ctx->dyn + 2) dd.epi.xnb = ctx->dyn_cur + 2;
+    if (dd.anb == ctx->dyn + 2) dd.anb = ctx->dyn_cur + 2;
     MV_CHECK(gemm_run(dd, ws, ctx->ws_elems, st));
     return MVAE_OK;
   }
@@ -1169,8 +1204,12 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
     // the previous one (its readers are all behind on this stream), no memset launch per step
     int* prev = c->dyn_cur ? c->dyn_cur : c->dyn;
     int* cur = c->dyn ? (prev == c->dyn ? c->dyn + 1 : c->dyn) : nullptr;
-    MV_CHECK(launch_deinterleave(x, c->xs, planes_of(c, c->xs), cur, c->dyn ? prev : nullptr, c->B,
-                                 c->D, c->ldx, c->x32mask, c->x32dyn, st, c->xbits, c->ldbits));
+    if (c->bits_on)  // the BitMats and target bits; the planes only for a batch not all 0 / 1
+      MV_CHECK(launch_deint_bits(x, c->B, c->D, c->xbf, c->kts_f, c->xbw, c->kts_w, c->xbits, c->ldbits, cur,
+                                 prev, c->xs, planes_of(c, c->xs), c->ldx, c->x32dyn, st));
+    else
+      MV_CHECK(launch_deinterleave(x, c->xs, planes_of(c, c->xs), cur, c->dyn ? prev : nullptr, c->B,
+                                   c->D, c->ldx, c->x32mask, c->x32dyn, st, c->xbits, c->ldbits));
     c->dyn_cur = cur;
   }
   if (c->diag_shadow && c->diag_shadow_at == 0 && draw == ENC_TRAIN) {
@@ -1719,6 +1758,17 @@ extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int
     d.Ap = A_.p; d.pA = A_.stride; d.nA = np;
     d.Bp = B_.p; d.pB = B_.stride; d.nB = np;
   }
+  // epi bit 14 (plane modes, A of 0/1 values): A also as a BitMat, the eight-phase kernel's bits path
+  if (e == hipSuccess && ((epi >> 14) & 1) && d.prec != GEMM_F32) {
+    void *pbits = nullptr, *pnb = nullptr;
+    const int kts = bitmat_kts(K);
+    e = hipMalloc(&pbits, bitmat_words(M, K) * 4);
+    if (e == hipSuccess) e = hipMalloc(&pnb, 16);
+    if (e == hipSuccess) tmp.push_back(pbits), tmp.push_back(pnb);
+    if (e == hipSuccess) e = hipMemsetAsync(pnb, 0, 16, st);
+    if (e == hipSuccess) e = launch_bits_from_plane(d.Ap, lda, at != 0, M, K, (unsigned*)pbits, kts, (int*)pnb, st);
+    d.Abits = (const unsigned*)pbits; d.abits_kts = kts; d.anb = (const int*)pnb;
+  }
   // epi bit 12 (plane modes): the output as bf16 planes only (no fp32 store), as the step's
   // producers write their operand images; C then receives the planes' sum (host side)
   const bool planes_out = ((epi >> 12) & 1) && d.prec != GEMM_F32;
@@ -1856,6 +1906,12 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   if (e == hipSuccess) e = launch_normal(A, 1, 1, (int)na, 1, 0, 1, 0, st);
   if (e == hipSuccess) e = launch_normal(Bm, 1, 1, (int)nb, 1, 0, 2, 0, st);
   d.A = A; d.B = Bm; d.C = Cm;
+  // variant bit 20: A of 0/1 values (the layer-0 pixels; in f32x its residual planes then zero);
+  // bit 21: ... and also as a BitMat per batch (the eight-phase kernel's bits path)
+  const bool bin = (variant >> 20) & 1, use_bits = bin && ((variant >> 21) & 1);
+  unsigned* bits = nullptr;
+  int* bnb = nullptr;
+  if (e == hipSuccess && bin) e = launch_binarize(A, na, st);
   if (e == hipSuccess && np) {
     e = hipMalloc(&planes, (size_t)np * (na + nb) * 2);
     Planes A_{planes, (long long)na, np}, B_{planes + np * na, (long long)nb, np};
@@ -1863,6 +1919,23 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
     if (e == hipSuccess) e = launch_split_planes(Bm, nb, B_, st);
     d.Ap = A_.p; d.pA = A_.stride; d.nA = np;
     d.Bp = B_.p; d.pB = B_.stride; d.nB = np;
+    if (bin && np == 3) {  // the step's pixel operand: residual planes zero, read from a zero flag
+      if (e == hipSuccess) e = hipMalloc(&bnb, 16);
+      if (e == hipSuccess) e = hipMemsetAsync(bnb, 0, 16, st);
+      d.dynA = bnb;
+    }
+    if (e == hipSuccess && use_bits) {
+      const int kts = bitmat_kts(K);
+      const size_t bw = bitmat_words(M, K);
+      if (!bnb) {
+        e = hipMalloc(&bnb, 16);
+        if (e == hipSuccess) e = hipMemsetAsync(bnb, 0, 16, st);
+      }
+      if (e == hipSuccess) e = hipMalloc(&bits, bw * batch * 4);
+      for (int b = 0; e == hipSuccess && b < batch; ++b)
+        e = launch_bits_from_plane(A_.p + (size_t)b * sa, lda, at != 0, M, K, bits + b * bw, kts, bnb + 2, st);
+      d.Abits = bits; d.abits_kts = kts; d.abits_sb = (long long)bw; d.anb = bnb + 2;
+    }
   }
   // epilogue (variant >> 8): the step's fused epilogues with their operand reads and the
   // output planes the next GEMM would read
@@ -2008,6 +2081,8 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
   if (planes) (void)hipFree(planes);
   if (cpl) (void)hipFree(cpl);
   if (xpl) (void)hipFree(xpl);
+  if (bits) (void)hipFree(bits);
+  if (bnb) (void)hipFree(bnb);
   if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
   return MVAE_OK;
 }

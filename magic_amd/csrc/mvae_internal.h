@@ -91,8 +91,33 @@ struct GemmDesc {
   // s_memrealtime stamps {start, prologue copy landed, k-loop done, end} (never in the step)
   unsigned long long* stamps = nullptr;
   int group = -1;                      // bf16 DMA kernels' tile order (Params::group); -1 planner
+  // A as bits (bf16 / f32x modes, a 0/1 operand: the layer-0 pixels): the BitMat below, read by
+  // the eight-phase kernel instead of A's planes while *anb == 0 (the de-interleave's not-binary
+  // word); strips of abits_kts blocks, batch stride abits_sb words. The planes stay the operand of
+  // every batch with a pixel other than 0 or 1.
+  const unsigned* Abits = nullptr;
+  int abits_kts = 0;
+  long long abits_sb = 0;
+  const int* anb = nullptr;
   GemmEpi epi;
 };
+
+// BitMat: a 0/1 GEMM operand A (logical [M][K], rows x k) at one bit per element, laid out for
+// the eight-phase kernel's 256 x 256 x 64 tiles and its 16x16x32 MFMA A fragments. Blocks of 256
+// rows x 64 k (2 KB = 512 words): block (mt, kt) at word 512 (mt kts + kt), kts >= ceil(K / 64)
+// blocks per 256-row strip. In a block, word 2 ((2 s + wm) 64 + lane) + j holds the 64-row
+// quarter (s, wm) of lane `lane`'s fragments: for row 128 s + 64 wm + 16 (2 j + h) + (lane & 15)
+// and k = 32 kh + 8 (lane >> 4) + el (h, kh in {0,1}, el < 8), bit 8 h + 4 kh + (el >> 1) +
+// 16 (el & 1) -- so the bf16 pair (el, el + 1) = (2 d, 2 d + 1) of fragment (2 j + h, kh) is
+// ((w >> 8 h) & (0x10001 << p)) * (0x3F80 >> p), p = 4 kh + d: two VALU operations per dword.
+// Rows >= M and k >= K are 0.
+constexpr int BITMAT_BLOCK_WORDS = 512;
+inline int bitmat_kts(int K) { return (K + 63) / 64; }
+inline size_t bitmat_words(int M, int K) { return (size_t)((M + 255) / 256) * bitmat_kts(K) * BITMAT_BLOCK_WORDS; }
+// (tests / diagnostics) a bf16 plane of 0/1 values -> BitMat: plane[row * ld + k], or
+// plane[k * ld + row] when trans (A stored [K][M]); *nb (optional) set if a value is not 0 or 1
+hipError_t launch_bits_from_plane(const unsigned short* plane, int ld, bool trans, int M, int K,
+                                  unsigned* out, int kts, int* nb, hipStream_t st);
 
 // Split-K choice for a GEMM (deterministic slab reduction when > 1).
 int gemm_plan_split(const GemmDesc& d, size_t max_ws);
@@ -157,6 +182,15 @@ struct Planes {
 hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int* dyn, int* dyn_next,
                                int B, int D, int ldx, int f32mask, int f32dyn_mask, hipStream_t st,
                                unsigned char* xbits = nullptr, int ldbits = 0);
+// The pixel operand of a 0/1 batch as bits (D % 8 == 0, B % 64 == 0): the forward BitMat xbf
+// (3B x (D + 1), kts_f = bitmat_kts(D + 1)), the weight-gradient BitMat xbw ((D + 1) x 3B, kts_w =
+// bitmat_kts(3B)) and the BCE target bits; *dyn slot 2 raised when a pixel is not 0 / 1, and then
+// (a gated second kernel) the planes of xp, the fp32 rows of f32dyn_mask and the inexact flag as
+// launch_deinterleave writes them. dyn_next: the other flag slot, zeroed. Both BitMats must be
+// zero-filled once (their padding is never written).
+hipError_t launch_deint_bits(const float* x, int B, int D, unsigned* xbf, int kts_f, unsigned* xbw, int kts_w,
+                             unsigned char* xbits, int ldbits, int* dyn, int* dyn_next, float* xs,
+                             const Planes& xp, int ldx, int f32dyn_mask, hipStream_t st);
 // (diagnostics) the bf16 plane-0 pass alone into xp: grid -1 the normal launch, > 0 that many
 // persistent 256-thread workgroups striding over the rows' 8-pixel groups
 hipError_t launch_deinterleave_grid(const float* x, unsigned short* xp, int B, int D, int ldx, int grid,

@@ -830,6 +830,154 @@ __global__ __launch_bounds__(256) void make_batch4_kernel(const unsigned char* _
   }
 }
 
+// ---------------------------------------------------------------- de-interleave to bits
+// The layer-0 pixel operand of a 0/1 batch as the eight-phase kernel's BitMats (mvae_internal.h):
+// xbf = A of the forward (rows [rot | lock | key] x pixels, the ones column at k = D), xbw = A of
+// the weight gradient (pixels x rows, the ones row at pixel D), plus the BCE target (the lock
+// block) as bits per row (GemmEpi::xbits) -- 1.1 bits written per pixel triple instead of the 48
+// of the bf16 plane. One workgroup: 64 batch rows x 128 pixels (two k-tiles / two 64-pixel
+// quarters). Each thread reads 4 x 96 contiguous bytes (8 pixels of one row, as the plane kernel),
+// writes one byte per block into LDS ([block][octet][row]: a row-contiguous 8 x 8 bit block is one
+// u64), then assembles 3 forward and 3 weight-gradient words, stored 512 B contiguous per block.
+// Raises the not-binary word (*dyn slot 2) when a pixel is neither 0 nor 1: the step then runs
+// deint_grey_kernel (the planes) and the GEMMs read the planes. Padding outside the written
+// blocks (rows past 3B, pixel quarters past D) is zero from the buffers' creation.
+// bits el = 0..7 of b -> positions 0..3 (even el) and 16..19 (odd el): a BitMat word's layout
+__device__ __forceinline__ unsigned bits_spread(unsigned b) {
+  unsigned e = b & 0x55u, o = (b >> 1) & 0x55u;
+  e = (e | (e >> 1)) & 0x33u; e = (e | (e >> 2)) & 0x0Fu;
+  o = (o | (o >> 1)) & 0x33u; o = (o | (o >> 2)) & 0x0Fu;
+  return e | (o << 16);
+}
+__global__ __launch_bounds__(256) void deint_bits_kernel(const float4* __restrict__ x, int B, int D, int kts_f,
+                                                         int kts_w, unsigned* __restrict__ xbf,
+                                                         unsigned* __restrict__ xbw,
+                                                         unsigned char* __restrict__ xbits, int ldbits,
+                                                         int* __restrict__ dyn, int* __restrict__ dyn_next) {
+  if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) dyn_next[0] = dyn_next[2] = 0;
+  __shared__ __attribute__((aligned(16))) unsigned char bt[3][16][64];  // [block][octet][row]
+  const int tid = threadIdx.x;
+  const int b0 = blockIdx.y * 64, p0 = blockIdx.x * 128;
+  const int o = tid & 15, pix = p0 + 8 * o;
+  const bool in = pix + 8 <= D;
+  float4 v[4][6];
+  if (in) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4* src = x + ((size_t)(b0 + (tid >> 4) + 16 * i) * 3 * D + 3 * (size_t)pix) / 4;
+#pragma unroll
+      for (int k = 0; k < 6; ++k) v[i][k] = src[k];
+    }
+  }
+  bool nb = false;
+  // pixels past D: the ones column (pixel D) and zeros
+  const unsigned pad = (pix <= D && D < pix + 8) ? 1u << (D - pix) : 0u;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (tid >> 4) + 16 * i;
+    unsigned by[3] = {pad, pad, pad};
+    if (in) {
+      const float e[24] = {v[i][0].x, v[i][0].y, v[i][0].z, v[i][0].w, v[i][1].x, v[i][1].y, v[i][1].z, v[i][1].w,
+                           v[i][2].x, v[i][2].y, v[i][2].z, v[i][2].w, v[i][3].x, v[i][3].y, v[i][3].z, v[i][3].w,
+                           v[i][4].x, v[i][4].y, v[i][4].z, v[i][4].w, v[i][5].x, v[i][5].y, v[i][5].z, v[i][5].w};
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int ch = c == 0 ? 1 : (c == 1 ? 0 : 2);  // block c (rot, lock, key) <- channel ch
+        unsigned byte = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float f = e[3 * j + ch];
+          byte |= (f != 0.f ? 1u : 0u) << j;
+          nb |= (f != 0.f) & (f != 1.f);
+        }
+        by[c] = byte;
+      }
+      xbits[(size_t)(b0 + r) * ldbits + (pix >> 3)] = (unsigned char)by[1];
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) bt[c][o][r] = (unsigned char)by[c];
+  }
+  if (dyn) {
+    const bool anb = __ballot(nb) != 0;
+    if ((tid & 63) == 0 && anb) atomicOr(dyn + 2, 1);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+    const int c = u;  // thread tid's word (kk, lane, j) of block c: 128 consecutive words per kk
+    const int kk = tid >> 7, wl = tid & 127, lane = wl >> 1, j = wl & 1;
+    const int grow = c * B + b0;  // first stacked row of this workgroup's 64
+    // forward: rows 16 (2 j + h) + (lane & 15), k-octet 8 kk + 4 kh + (lane >> 4)
+    const int kt = 2 * blockIdx.x + kk;
+    if (kt < kts_f) {
+      unsigned w = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+          w |= bits_spread(bt[c][8 * kk + 4 * kh + (lane >> 4)][16 * (2 * j + h) + (lane & 15)]) << (8 * h + 4 * kh);
+      xbf[((size_t)(grow >> 8) * kts_f + kt) * BITMAT_BLOCK_WORDS + ((grow >> 6) & 3) * 128 + wl] = w;
+    }
+    // weight gradient: pixel 64 kk + 16 (2 j + h) + (lane & 15) of this block's 128, rows
+    // 32 kh + 8 (lane >> 4) + 0..7 -- bit (pixel & 7) of 8 row bytes of one octet
+    const int pq = p0 + 64 * kk;
+    if (pq <= D) {
+      unsigned w = 0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh) {
+          const int pr = 64 * kk + 16 * (2 * j + h) + (lane & 15);
+          const unsigned long long rows =
+              *reinterpret_cast<const unsigned long long*>(&bt[c][pr >> 3][32 * kh + 8 * (lane >> 4)]);
+          const unsigned long long col = (rows >> (pr & 7)) & 0x0101010101010101ull;
+          const unsigned byte = (unsigned)((col * 0x0102040810204080ull) >> 56);  // bit i = row i
+          w |= bits_spread(byte) << (8 * h + 4 * kh);
+        }
+      xbw[((size_t)(pq >> 8) * kts_w + (grow >> 6)) * BITMAT_BLOCK_WORDS + ((pq >> 6) & 3) * 128 + wl] = w;
+    }
+  }
+}
+
+// The plane image of a batch with a pixel other than 0 or 1 (after deint_bits_kernel raised the
+// not-binary word; else every workgroup returns at once): bf16 plane 0 (planes 1-2 of the exact
+// split too when np == 3), the fp32 rows of the blocks in f32mask, and the inexact flag (*dyn) --
+// what the plane path's GEMMs and the BCE epilogue read. Workgroups stride over the 8-pixel groups.
+__global__ void deint_grey_kernel(const float4* __restrict__ x, float* __restrict__ xs,
+                                  unsigned short* __restrict__ xp, long long ps, int np, int f32mask,
+                                  int* __restrict__ dyn, int B, int D, int ldx) {
+  if (dyn[2] == 0) return;
+  const int nq = D / 8;
+  const size_t n = (size_t)B * nq;
+  bool nz = false;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int b = (int)(i / nq), q = (int)(i % nq);
+    const float4* src = x + ((size_t)b * 3 * D) / 4 + 6 * (size_t)q;
+    float4 v[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v[k] = src[k];
+    nz |= deint_put<2>(v, xs, xp, B, b, (size_t)8 * q, ldx, f32mask);
+    if (np == 3) {  // the exact split's residual planes of the 24 values
+      const float e[24] = {v[0].x, v[0].y, v[0].z, v[0].w, v[1].x, v[1].y, v[1].z, v[1].w,
+                           v[2].x, v[2].y, v[2].z, v[2].w, v[3].x, v[3].y, v[3].z, v[3].w,
+                           v[4].x, v[4].y, v[4].z, v[4].w, v[5].x, v[5].y, v[5].z, v[5].w};
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const int ch = c == 0 ? 1 : (c == 1 ? 0 : 2);
+        const size_t o = (size_t)(c * B + b) * ldx + (size_t)8 * q;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          float r1, r2, r3;
+          (void)bf16_rn(e[3 * j + ch], r1);
+          xp[ps + o + j] = bf16_rn(r1, r2);
+          xp[2 * ps + o + j] = bf16_rn(r2, r3);
+        }
+      }
+    }
+  }
+  if (__ballot(nz) != 0 && (threadIdx.x & 63) == 0) atomicOr(dyn, 1);
+}
+
 inline unsigned nblocks(size_t n, int bs) { return (unsigned)((n + bs - 1) / bs); }
 
 __global__ void mvae_region_marker() {}
@@ -860,6 +1008,20 @@ hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int*
   if (dyn && xp.p && (xp.n == 3 || f32dyn_mask))
     hipLaunchKernelGGL(residual_planes_kernel, dim3(2048), dim3(256), 0, st, x, xs, xp.p, xp.stride,
                        xp.n, f32dyn_mask, dyn, B, D, ldx);
+  return hipGetLastError();
+}
+
+hipError_t launch_deint_bits(const float* x, int B, int D, unsigned* xbf, int kts_f, unsigned* xbw, int kts_w,
+                             unsigned char* xbits, int ldbits, int* dyn, int* dyn_next, float* xs,
+                             const Planes& xp, int ldx, int f32dyn_mask, hipStream_t st) {
+  if ((D % 8) || (B % 64) || (reinterpret_cast<uintptr_t>(x) % 16) || (ldx % 8) || !dyn || !xp.p ||
+      kts_f != bitmat_kts(D + 1) || kts_w != bitmat_kts(3 * B))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(deint_bits_kernel, dim3((kts_f + 1) / 2, B / 64), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(x), B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn,
+                     dyn_next);
+  hipLaunchKernelGGL(deint_grey_kernel, dim3(1024), dim3(256), 0, st, reinterpret_cast<const float4*>(x), xs,
+                     xp.p, xp.stride, xp.n, f32dyn_mask, dyn, B, D, ldx);
   return hipGetLastError();
 }
 

@@ -64,7 +64,16 @@ def main():
     torch.cuda.init()
     st = torch.cuda.current_stream().cuda_stream
     cfg = baseline_config(args.config)
-    variants = [(int(v), int(d)) for v in args.variants.split(",") for d in args.diag.split(",")]
+    # a variant may end in "b" (A of 0/1 values: the layer-0 pixels) or "B" (... and read as a
+    # BitMat by the eight-phase kernel's bits path): mvae_bench_gemm variant bits 20 / 21
+    def vparse(v):
+        f = 0
+        if v.endswith("b"):
+            v, f = v[:-1], 1 << 20
+        elif v.endswith("B"):
+            v, f = v[:-1], 3 << 20
+        return int(v) | f
+    variants = [(vparse(v), int(d)) for v in args.variants.split(",") for d in args.diag.split(",")]
     want = set(args.shapes.split(",")) if args.shapes else None
     extra = []
     for e in args.extra:
@@ -81,7 +90,7 @@ def main():
                 if rc != 0:
                     raise RuntimeError(lib.mvae_last_error(None))
                 res.setdefault((name, v), []).append(ms.value)
-    lab = [f"v{v}" + (f"d{d}" if d else "") for v, d in variants]
+    lab = [f"v{v & 0xfffff}" + {0: "", 1: "b", 3: "B"}[v >> 20] + (f"d{d}" if d else "") for v, d in variants]
     print(f"{'shape':16s} {'MxNxK':>22s} batch " + " ".join(f"{x + ' TF/s':>12s}" for x in lab))
     for name, M, N, K, at, bt, batch, epi in sh:
         fl = 2.0 * M * N * K * batch
