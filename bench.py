@@ -526,6 +526,35 @@ def dry_run_batch(cfg, world, rank, j):
 
 
 # ------------------------------------------------------------------------ measurement
+def allreduce_bench(eng, dev, world, dry_run, reps=5):
+    """The achieved rate of one all-reduce of the step's whole gradient bucket (the [g1 | g2]
+    buffer's size, fp32) on its own: mean time over reps, algorithm bandwidth and bus bandwidth
+    (2 (N - 1) / N x bytes / time, the ring all-reduce's per-link traffic)."""
+    import torch
+    import torch.distributed as dist
+    n = eng.grads.numel()
+    t = torch.ones(n, dtype=eng.grads.dtype, device=dev)
+    dist.all_reduce(t)
+    dist.barrier()
+    if dry_run:
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            dist.all_reduce(t)
+        ms = (time.perf_counter() - t0) * 1e3 / reps
+    else:
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            dist.all_reduce(t)
+        b.record()
+        b.synchronize()
+        ms = a.elapsed_time(b) / reps
+    nbytes = n * t.element_size()
+    return {"bytes": nbytes, "ms": round(ms, 4), "algbw_GBps": round(nbytes / (ms * 1e-3) / 1e9, 5),
+            "busbw_GBps": round(2 * (world - 1) / world * nbytes / (ms * 1e-3) / 1e9, 5)}
+
+
 def measure(args, cfg, world, rank, local, dev, *, timing, steps, warmup, keep=False, h2d=False,
             pipeline=False):
     """One configuration through the training step: W warm-up steps, a region pass (HIP events
@@ -609,7 +638,13 @@ def measure(args, cfg, world, rank, local, dev, *, timing, steps, warmup, keep=F
             el = float(t.item())
         return el
 
+    stepper.comm_timing = world > 1  # exposed collective waits of the timed steps
     elapsed = timed(steps, lambda i: pool[i % 2])
+    stepper.comm_timing = False
+    comm = None
+    if world > 1:
+        comm = stepper.comm_stats()
+        comm["allreduce_bench"] = allreduce_bench(eng, dev, world, args.dry_run)
     dom_timed = None
     if timing:
         eng.timing_enable(False)
@@ -620,7 +655,7 @@ def measure(args, cfg, world, rank, local, dev, *, timing, steps, warmup, keep=F
         raise RuntimeError(f"non-finite losses after the timed steps: {losses}")
     out = {"cfg": cfg, "elapsed": elapsed, "host_elapsed": host_t[0], "steps": steps,
            "regions": regions, "dom": dom,
-           "dom_timed": dom_timed, "losses": losses}
+           "dom_timed": dom_timed, "losses": losses, "comm": comm}
     if not args.dry_run:
         out["n_all"] = eng.buffer(_lib.BUF_PARAMS).numel()
         out["n_enc"] = eng.buffer(_lib.BUF_GRADS).numel() - out["n_all"]
@@ -970,6 +1005,7 @@ def main():
                               "host_ms_per_step": round(m["host_elapsed"] / m["steps"] * 1e3, 4),
                               "global_batch": c.batch * world, "per_gpu_batch": c.batch,
                               "dtype": c.precision, "overlap_mse": round(m["mse"], 2),
+                              "comm": m.get("comm"),
                               "roofline": rf, "loss_roofline": lr, "pipeline": m.get("pipeline")}
 
     if rank == 0:
@@ -1032,6 +1068,10 @@ def main():
             "h2d": head.get("h2d"),
             "pipeline": head.get("pipeline"),
             "configs": extra,
+            # N > 1: per-step exposed wait of the gradient all-reduces and blocking statistics
+            # all-reduces (HIP events on the step's stream), bucket bytes, and one all-reduce of
+            # the bucket's size on its own (bus bandwidth)
+            "comm": head.get("comm"),
             "build_id": None if args.dry_run else _lib.load().mvae_build_id().decode(),
         }
         if args.dry_run:

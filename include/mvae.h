@@ -195,7 +195,8 @@ int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* cou
  * parameters, their Adam state and MVAE_BUF_GRADS are not to be read between mvae_backward and
  * mvae_adam; 1: one GEMM, everything in mvae_adam); "bce_split" (default 1) runs a BCE head whose
  * 256x256 tiles leave a partial last round as the whole rounds plus 256x128 tiles for the rest
- * (the same results); "side_mask" (0-3, default 3): which weight gradients run on the side
+ * (bitwise the same results in bf16; in f32x equal to fp32 rounding: the two kernels sum the plane
+ * pairs in different orders); "side_mask" (0-3, default 3): which weight gradients run on the side
  * stream -- bit 0 the decoder's, bit 1 the encoder's (a cleared bit: in order on the caller's
  * stream; the same results). */
 int mvae_set_option(mvae_ctx* ctx, const char* name, int value);
@@ -252,6 +253,10 @@ int mvae_timing_reset(mvae_ctx* ctx);
  * (synchronous; tests only). mvae_bench_gemm: variant | (prec << 4) | (epi << 8).    */
 int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, int variant, int iters,
                     void* stream, float* avg_ms);
+/* Diagnostics: the step's de-interleave of a [B][3D] batch of random 0/1 pixels, iters launches
+ * (B % 64 == 0, D % 8 == 0): variant 0-4 the bits forms (the pixel operand as BitMats), 100 the
+ * bf16-plane pass. Average ms per launch in *avg_ms.                                         */
+int mvae_bench_deint(int B, int D, int variant, int iters, void* stream, float* avg_ms);
 /* One 5x5x64x64 conv kernel of the conv tower on caller data (tests; synchronous): S1 x S1 x 64
  * NHWC images, B rows (3B forward images, 4B backward). mode 0: relu(conv(x, W2) + b2), 3B
  * images, y = W2 block [1601][64]; mode 1: data gradient of x (4B images), y = W2; mode 2:

@@ -94,6 +94,7 @@ _SIGS = {
     "mvae_timing_reset": ([C.c_void_p], C.c_int),
     "mvae_bench_gemm": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                          C.c_void_p, C.POINTER(C.c_float)], C.c_int),
+    "mvae_bench_deint": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_float)], C.c_int),
     "mvae_debug_conv2": ([C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
                           C.c_void_p], C.c_int),
     "mvae_debug_gemm": ([C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_void_p,

@@ -26,7 +26,7 @@ struct Params {
                             // walked n by n, so an XCD's resident tiles share A and B in its L2
   GemmEpi epi;
 };
-constexpr int TN_E8 = 2;    // Params::tn of the 256 x 256 eight-phase kernel (gemm_bf16e.hip)
+constexpr int TN_E8 = GEMM_TN_E8;  // Params::tn of the 256 x 256 eight-phase kernel (gemm_bf16e.hip)
 
 // launch parameters of the bf16-plane kernels (gemm_bf16.hip, gemm_bf16e.hip)
 struct PParams {
@@ -51,6 +51,8 @@ struct PParams {
   long long abits_sb = 0;
   const int* anb = nullptr;
   int npairs_a0 = 1;                // the leading pairs with A plane 0 (the bits path's pairs)
+  int bits_mode = 2;                // bits path: 1 fragments expanded in registers per wave, 2 the A
+                                    // images expanded once per workgroup (gemm_bf16e.hip E8)
 };
 
 // tanh as an odd [13/6] rational in x on [-7.905, 7.905] (clamped beyond, where tanh rounds to

@@ -844,8 +844,18 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
       c->bits_on = true;
     }
   }
-  {  // layer-0 weight-gradient row chunks (see w0c): the wired GEMM re-pointed at row ranges
+  {  // layer-0 weight-gradient row chunks (see w0c): the wired GEMM re-pointed at row ranges,
+     // with the whole GEMM's split-K and kernel pinned, so each output row is summed exactly as
+     // the one-GEMM backward sums it (chunked and unchunked backwards are bitwise equal: the early
+     // Adam's chunks, the data-parallel parts)
     const GemmDesc& w = c->bwd_enc[c->nenc];
+    const int w_split = gemm_plan_split(w, ~size_t(0));
+    int w_variant = w.variant;
+    if (w.prec != GEMM_F32 && !w.valu && gemm_bf16_wide(w) && w.variant == 0) {
+      int sp = 0, tn = 0, tm = 0;
+      gemm_bf16_wide_plan(w, ~size_t(0), &sp, &tn, &tm);
+      w_variant = tn == GEMM_TN_E8 ? 13 : (tn == 128 ? 11 : 12);  // (tm: 256 for an A^T operand)
+    }
     for (int R : {2, 4, 8}) {
       const int per = ((w.M + R - 1) / R + 255) / 256 * 256;
       for (int m0 = 0; m0 < w.M; m0 += per) {
@@ -856,6 +866,8 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
         if (d.Ap) d.Ap = w.Ap + m0;
         d.C = w.C + (size_t)m0 * w.ldc;  // output rows
         if (d.Abits) d.Abits = w.Abits + (size_t)(m0 / 256) * w.abits_kts * BITMAT_BLOCK_WORDS;
+        d.split = w_split;
+        d.variant = w_variant;
         c->w0c[R].push_back(d);
         c->w0m[R].push_back(m0);
       }
@@ -982,7 +994,14 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
     }
     for (int i = 0; se == hipSuccess && i < 16; ++i) {
       hipEvent_t ev = nullptr;
-      // stream-to-stream ordering on this device only: no system-scope fence
+      // stream-to-stream ordering on this device only: no system-scope fence. The producer side
+      // of every fork / join is a kernel, and a kernel's end-of-dispatch release is at least agent
+      // scope -- the whole device, every XCD's L2 written back -- which is what a consumer kernel
+      // on another queue of the same device needs; system scope adds only host / peer visibility,
+      // which nothing here reads through these events (they order GPU work; the host waits on
+      // stream / device synchronisation, which keeps its own fences). Measured: -0.009 ms per step
+      // at C2 / C3 (profiles/r5/r5z_events_without_system_fence.txt); the bitwise tests of the
+      // side-stream schedules (test_gpu_r2.py early Adam, side_mask) run with these events.
       se = hipEventCreateWithFlags(&ev, hipEventDisableTiming | hipEventDisableSystemFence);
       if (se == hipSuccess) c->sync_ev.push_back(ev);
     }
@@ -1480,6 +1499,7 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
     if (c->early_adam && two && !join_dec) {
       if ((rc = fork())) return rc;
       c->early_fork = true;
+      c->side_pending = true;  // (if mvae_adam never comes, the next encode() joins the side stream)
     }
     if ((rc = w0chunk(0))) return rc;
     if ((rc = chunk_adam(0))) return rc;
@@ -1768,6 +1788,7 @@ extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int
     if (e == hipSuccess) e = hipMemsetAsync(pnb, 0, 16, st);
     if (e == hipSuccess) e = launch_bits_from_plane(d.Ap, lda, at != 0, M, K, (unsigned*)pbits, kts, (int*)pnb, st);
     d.Abits = (const unsigned*)pbits; d.abits_kts = kts; d.anb = (const int*)pnb;
+    if ((epi >> 15) & 1) d.bits_mode = 1;  // epi bit 15: fragments expanded per wave
   }
   // epi bit 12 (plane modes): the output as bf16 planes only (no fp32 store), as the step's
   // producers write their operand images; C then receives the planes' sum (host side)
@@ -1874,6 +1895,54 @@ extern "C" int mvae_timing_reset(mvae_ctx* ctx) {
 // Time one GEMM shape of the step's kernel family (diagnostics): operands are allocated
 // and filled with uniform [-1,1) values inside, `iters` launches are timed with HIP events
 // on `stream` after 3 warm-ups. variant selects a kernel variant (0 = default).
+// (diagnostics) the de-interleave of a [B][3D] batch of random 0/1 pixels (density 0.1), iters
+// launches on the stream: variant 0-4 the bits forms (launch_deint_bits), 100 the bf16-plane pass
+extern "C" int mvae_bench_deint(int B, int D, int variant, int iters, void* stream, float* avg_ms) {
+  if (B <= 0 || D <= 0 || B % 64 || D % 8 || iters <= 0 || !avg_ms) return MVAE_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  const int ldx = (D + 1 + 7) / 8 * 8, ldbits = (D / 8 + 15) & ~15;
+  const int kf = bitmat_kts(D + 1), kw = bitmat_kts(3 * B);
+  std::vector<void*> m;
+  auto al = [&](size_t bytes) -> void* {
+    void* q = nullptr;
+    if (hipMalloc(&q, bytes) != hipSuccess) return nullptr;
+    (void)hipMemsetAsync(q, 0, bytes, st);
+    m.push_back(q);
+    return q;
+  };
+  float* x = (float*)al((size_t)B * 3 * D * 4);
+  float* xs = (float*)al((size_t)3 * B * ldx * 4);
+  unsigned short* xp = (unsigned short*)al((size_t)3 * B * ldx * 2);
+  unsigned* xbf = (unsigned*)al(bitmat_words(3 * B, D + 1) * 4);
+  unsigned* xbw = (unsigned*)al(bitmat_words(D + 1, 3 * B) * 4);
+  unsigned char* xb = (unsigned char*)al((size_t)B * ldbits);
+  int* dyn = (int*)al(64);
+  hipError_t e = (x && xs && xp && xbf && xbw && xb && dyn) ? hipSuccess : hipErrorOutOfMemory;
+  if (e == hipSuccess) e = launch_normal(x, 1, 1, B * 3 * D, 1, 0, 5, 0, st);
+  if (e == hipSuccess) e = launch_binarize(x, (size_t)B * 3 * D, st);  // x > 0: half the pixels 1
+  const Planes pl{xp, (long long)3 * B * ldx, 1};
+  auto one = [&]() -> hipError_t {
+    if (variant == 100) return launch_deinterleave(x, xs, pl, dyn, dyn + 4, B, D, ldx, 0, 2, st, xb, ldbits);
+    return launch_deint_bits(x, B, D, xbf, kf, xbw, kw, xb, ldbits, dyn, dyn + 4, xs, pl, ldx, 2, st, variant);
+  };
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  if (e == hipSuccess) e = hipEventCreate(&t0);
+  if (e == hipSuccess) e = hipEventCreate(&t1);
+  for (int i = 0; e == hipSuccess && i < 3; ++i) e = one();
+  if (e == hipSuccess) e = hipEventRecord(t0, st);
+  for (int i = 0; e == hipSuccess && i < iters; ++i) e = one();
+  if (e == hipSuccess) e = hipEventRecord(t1, st);
+  if (e == hipSuccess) e = hipEventSynchronize(t1);
+  float ms = 0.f;
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, t0, t1);
+  *avg_ms = ms / iters;
+  if (t0) (void)hipEventDestroy(t0);
+  if (t1) (void)hipEventDestroy(t1);
+  for (void* q : m) (void)hipFree(q);
+  if (e != hipSuccess) { g_create_err = hipGetErrorString(e); return (int)e; }
+  return MVAE_OK;
+}
+
 extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, int variant, int iters,
                                void* stream, float* avg_ms) {
   if (M <= 0 || N <= 0 || K <= 0 || iters <= 0 || !avg_ms || batch <= 0) return MVAE_EINVAL;
@@ -1935,6 +2004,7 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
       for (int b = 0; e == hipSuccess && b < batch; ++b)
         e = launch_bits_from_plane(A_.p + (size_t)b * sa, lda, at != 0, M, K, bits + b * bw, kts, bnb + 2, st);
       d.Abits = bits; d.abits_kts = kts; d.abits_sb = (long long)bw; d.anb = bnb + 2;
+      if ((variant >> 22) & 1) d.bits_mode = 1;  // bit 22: fragments expanded per wave
     }
   }
   // epilogue (variant >> 8): the step's fused epilogues with their operand reads and the

@@ -13,9 +13,10 @@ enum EpiMode {
   EPI_DACT = 2,     // C = acc * act'(aux[remap(row)])  (dgrad through the producing activation)
   EPI_BCE = 3,      // sigmoid + reconstruction BCE row partials + dU = (y - x) * scale (+ optional y)
   EPI_SIGMOID = 4,  // C = sigmoid(acc)                 (generate / reconstruct)
-  EPI_BCEB = 5,     // EPI_BCE reading the target from its bf16 plane (kernel-internal: gemm_run
-                    // launches EPI_BCE and EPI_BCEB and each returns at once unless *xdyn
-                    // selects it -- a runtime choice inside one epilogue spills the accumulators)
+  EPI_BCEB = 5,     // EPI_BCE whose target form the epilogue chooses at run time (kernel-
+                    // internal: gemm_run makes one EPI_BCEB launch when the target has a bf16
+                    // plane): its bits while *xnb == 0 (GemmEpi::xbits), its bf16 plane while
+                    // *xdyn == 0, else the fp32 rows (bce_x16 / epi_skip in gemm_common.h)
   EPI_DACTB = 6,    // EPI_DACT reading aux from its bf16 plane auxp (kernel-internal: the wide
                     // bf16 kernels' instantiation when auxp is set, so the fp32-aux path and its
                     // registers are not compiled into it)
@@ -99,6 +100,7 @@ struct GemmDesc {
   int abits_kts = 0;
   long long abits_sb = 0;
   const int* anb = nullptr;
+  int bits_mode = 2;                   // 1: fragments expanded per wave, 2: A images per workgroup
   GemmEpi epi;
 };
 
@@ -142,6 +144,7 @@ int gemm_bf16_wide_tm(const GemmDesc& d, size_t max_ws);
 void gemm_bf16_wide_plan(const GemmDesc& d, size_t max_ws, int* split, int* tn, int* tm);
 // Number of column blocks the BCE epilogue writes per row (rowpart's inner dim).
 int gemm_bce_nblk(int N);
+constexpr int GEMM_TN_E8 = 2;  // gemm_bf16_wide_plan's tile N of the eight-phase kernel (gemm::TN_E8)
 
 // ---- the encoder's hidden layers in one launch (enc_chain.hip, bf16 planes) ----
 // layer: out = act(in W) on bf16 planes; W [K][ldw] (K incl. the bias row), N output columns,
@@ -190,7 +193,7 @@ hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int*
 // zero-filled once (their padding is never written).
 hipError_t launch_deint_bits(const float* x, int B, int D, unsigned* xbf, int kts_f, unsigned* xbw, int kts_w,
                              unsigned char* xbits, int ldbits, int* dyn, int* dyn_next, float* xs,
-                             const Planes& xp, int ldx, int f32dyn_mask, hipStream_t st);
+                             const Planes& xp, int ldx, int f32dyn_mask, hipStream_t st, int variant = 0);
 // (diagnostics) the bf16 plane-0 pass alone into xp: grid -1 the normal launch, > 0 that many
 // persistent 256-thread workgroups striding over the rows' 8-pixel groups
 hipError_t launch_deinterleave_grid(const float* x, unsigned short* xp, int B, int D, int ldx, int grid,

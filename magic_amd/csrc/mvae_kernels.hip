@@ -849,22 +849,29 @@ __device__ __forceinline__ unsigned bits_spread(unsigned b) {
   o = (o | (o >> 1)) & 0x33u; o = (o | (o >> 2)) & 0x0Fu;
   return e | (o << 16);
 }
-__global__ __launch_bounds__(256) void deint_bits_kernel(const float4* __restrict__ x, int B, int D, int kts_f,
-                                                         int kts_w, unsigned* __restrict__ xbf,
-                                                         unsigned* __restrict__ xbw,
-                                                         unsigned char* __restrict__ xbits, int ldbits,
-                                                         int* __restrict__ dyn, int* __restrict__ dyn_next) {
+// PB k-tiles (64 PB pixels) per workgroup of NT threads; OS: LDS bytes per octet row (72: the 16
+// octets of a write land on 16 banks)
+template <int PB, int NT, int OS>
+__global__ __launch_bounds__(NT) void deint_bits_kernel(const float4* __restrict__ x, int B, int D, int kts_f,
+                                                        int kts_w, unsigned* __restrict__ xbf,
+                                                        unsigned* __restrict__ xbw,
+                                                        unsigned char* __restrict__ xbits, int ldbits,
+                                                        int* __restrict__ dyn, int* __restrict__ dyn_next) {
+  constexpr int NO = 8 * PB;          // octets per row
+  constexpr int RPP = NT / NO;        // rows per pass
+  constexpr int NR = 64 / RPP;        // row passes per thread
+  static_assert(NT % NO == 0 && 64 % RPP == 0, "whole rows per pass");
   if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) dyn_next[0] = dyn_next[2] = 0;
-  __shared__ __attribute__((aligned(16))) unsigned char bt[3][16][64];  // [block][octet][row]
+  __shared__ __attribute__((aligned(16))) unsigned char bt[3][NO][OS];  // [block][octet][row]
   const int tid = threadIdx.x;
-  const int b0 = blockIdx.y * 64, p0 = blockIdx.x * 128;
-  const int o = tid & 15, pix = p0 + 8 * o;
+  const int b0 = blockIdx.y * 64, p0 = blockIdx.x * 64 * PB;
+  const int o = tid % NO, pix = p0 + 8 * o;
   const bool in = pix + 8 <= D;
-  float4 v[4][6];
+  float4 v[NR][6];
   if (in) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float4* src = x + ((size_t)(b0 + (tid >> 4) + 16 * i) * 3 * D + 3 * (size_t)pix) / 4;
+    for (int i = 0; i < NR; ++i) {
+      const float4* src = x + ((size_t)(b0 + tid / NO + RPP * i) * 3 * D + 3 * (size_t)pix) / 4;
 #pragma unroll
       for (int k = 0; k < 6; ++k) v[i][k] = src[k];
     }
@@ -873,8 +880,8 @@ __global__ __launch_bounds__(256) void deint_bits_kernel(const float4* __restric
   // pixels past D: the ones column (pixel D) and zeros
   const unsigned pad = (pix <= D && D < pix + 8) ? 1u << (D - pix) : 0u;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int r = (tid >> 4) + 16 * i;
+  for (int i = 0; i < NR; ++i) {
+    const int r = tid / NO + RPP * i;
     unsigned by[3] = {pad, pad, pad};
     if (in) {
       const float e[24] = {v[i][0].x, v[i][0].y, v[i][0].z, v[i][0].w, v[i][1].x, v[i][1].y, v[i][1].z, v[i][1].w,
@@ -902,13 +909,12 @@ __global__ __launch_bounds__(256) void deint_bits_kernel(const float4* __restric
     if ((tid & 63) == 0 && anb) atomicOr(dyn + 2, 1);
   }
   __syncthreads();
-#pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int c = u;  // thread tid's word (kk, lane, j) of block c: 128 consecutive words per kk
-    const int kk = tid >> 7, wl = tid & 127, lane = wl >> 1, j = wl & 1;
+  // 3 blocks x PB (k-tiles / pixel quarters) x 128 words of each BitMat
+  for (int wi = tid; wi < 3 * PB * 128; wi += NT) {
+    const int c = wi / (PB * 128), kk = (wi / 128) % PB, wl = wi & 127, lane = wl >> 1, j = wl & 1;
     const int grow = c * B + b0;  // first stacked row of this workgroup's 64
     // forward: rows 16 (2 j + h) + (lane & 15), k-octet 8 kk + 4 kh + (lane >> 4)
-    const int kt = 2 * blockIdx.x + kk;
+    const int kt = PB * blockIdx.x + kk;
     if (kt < kts_f) {
       unsigned w = 0;
 #pragma unroll
@@ -918,7 +924,7 @@ __global__ __launch_bounds__(256) void deint_bits_kernel(const float4* __restric
           w |= bits_spread(bt[c][8 * kk + 4 * kh + (lane >> 4)][16 * (2 * j + h) + (lane & 15)]) << (8 * h + 4 * kh);
       xbf[((size_t)(grow >> 8) * kts_f + kt) * BITMAT_BLOCK_WORDS + ((grow >> 6) & 3) * 128 + wl] = w;
     }
-    // weight gradient: pixel 64 kk + 16 (2 j + h) + (lane & 15) of this block's 128, rows
+    // weight gradient: pixel 64 kk + 16 (2 j + h) + (lane & 15) of this block's, rows
     // 32 kh + 8 (lane >> 4) + 0..7 -- bit (pixel & 7) of 8 row bytes of one octet
     const int pq = p0 + 64 * kk;
     if (pq <= D) {
@@ -1013,13 +1019,32 @@ hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int*
 
 hipError_t launch_deint_bits(const float* x, int B, int D, unsigned* xbf, int kts_f, unsigned* xbw, int kts_w,
                              unsigned char* xbits, int ldbits, int* dyn, int* dyn_next, float* xs,
-                             const Planes& xp, int ldx, int f32dyn_mask, hipStream_t st) {
+                             const Planes& xp, int ldx, int f32dyn_mask, hipStream_t st, int variant) {
   if ((D % 8) || (B % 64) || (reinterpret_cast<uintptr_t>(x) % 16) || (ldx % 8) || !dyn || !xp.p ||
       kts_f != bitmat_kts(D + 1) || kts_w != bitmat_kts(3 * B))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(deint_bits_kernel, dim3((kts_f + 1) / 2, B / 64), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(x), B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn,
-                     dyn_next);
+  const float4* x4 = reinterpret_cast<const float4*>(x);
+  switch (variant) {  // (diagnostics: mvae_bench_deint) 0 = the step's form
+    case 1:
+      hipLaunchKernelGGL((deint_bits_kernel<2, 256, 64>), dim3((kts_f + 1) / 2, B / 64), dim3(256), 0, st, x4, B, D,
+                         kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
+      break;
+    case 2:
+      hipLaunchKernelGGL((deint_bits_kernel<4, 512, 72>), dim3((kts_f + 3) / 4, B / 64), dim3(512), 0, st, x4, B, D,
+                         kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
+      break;
+    case 3:
+      hipLaunchKernelGGL((deint_bits_kernel<1, 256, 72>), dim3(kts_f, B / 64), dim3(256), 0, st, x4, B, D,
+                         kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
+      break;
+    case 4:
+      hipLaunchKernelGGL((deint_bits_kernel<4, 256, 72>), dim3((kts_f + 3) / 4, B / 64), dim3(256), 0, st, x4, B, D,
+                         kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
+      break;
+    default:
+      hipLaunchKernelGGL((deint_bits_kernel<2, 256, 72>), dim3((kts_f + 1) / 2, B / 64), dim3(256), 0, st, x4, B, D,
+                         kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
+  }
   hipLaunchKernelGGL(deint_grey_kernel, dim3(1024), dim3(256), 0, st, reinterpret_cast<const float4*>(x), xs,
                      xp.p, xp.stride, xp.n, f32dyn_mask, dyn, B, D, ldx);
   return hipGetLastError();

@@ -22,11 +22,14 @@ Per step and rank (``world`` ranks, local batch B, global batch N*B):
 
 The squared-difference metric needs no mid-step collective; the result equals the
 single-process step on the concatenated batch (tests/test_parallel_gloo.py) to fp32
-rounding: with more than one rank the layer-0 weight gradient runs as ``wgrad0_chunks`` row
-chunks (engine option, set here and restored by ``close()``), whose GEMMs plan their own
-split-K, so those rows are not bitwise equal to a single-process one-GEMM backward.
+rounding (the rows are summed in another order across ranks). With more than one rank the
+layer-0 weight gradient runs as ``wgrad0_chunks`` row chunks (engine option, set here and
+restored by ``close()``); the chunk GEMMs keep the one-GEMM plan, so chunking alone changes no
+bit of a rank's gradients.
 """
 from __future__ import annotations
+
+import time
 
 import torch
 import torch.distributed as dist
@@ -79,6 +82,56 @@ class DataParallelStep:
             # the internal eps sampler draws this rank's rows of the global batch's stream,
             # so a sharded step without explicit eps equals the single-process step too
             engine.set_shard(self.rank * engine.cfg.batch)
+        # communication timing (comm_stats): off by default; bench.py turns it on for the timed
+        # loop of an N-rank run
+        self.comm_timing = False
+        self._marks = []          # per step: (blocking collectives [(t0, t1)], (t0, t1) of the wait)
+        self._bucket_bytes = 0
+        self._n_coll = 0
+
+    # a timestamp on the step's stream: a HIP event (recorded, read after a sync) or, for the CPU
+    # (gloo) path, the host clock (gloo's waits block the host)
+    def _mark(self):
+        if not self.comm_timing:
+            return None
+        if self.grads_on_gpu():
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ev
+        return time.perf_counter()
+
+    def grads_on_gpu(self) -> bool:
+        return getattr(self.e.grads, "is_cuda", False)
+
+    @staticmethod
+    def _ms(a, b) -> float:
+        if isinstance(a, float):
+            return (b - a) * 1e3
+        return a.elapsed_time(b)
+
+    def comm_stats(self) -> dict:
+        """Per-step communication figures of the steps run with comm_timing on (call after a
+        device sync): the exposed wait of the gradient all-reduces (the step's stream from the end
+        of the backward's launches until every bucket's all-reduce is done), the blocking cosine
+        statistics all-reduces, the bucket bytes and collective count. Clears the record."""
+        n = len(self._marks)
+        if n == 0:
+            return {}
+        wait = sum(self._ms(*m[1]) for m in self._marks) / n
+        blk = sum(sum(self._ms(a, b) for a, b in m[0]) for m in self._marks) / n
+        out = {"steps": n, "exposed_allreduce_wait_ms": round(wait, 4),
+               "blocking_stats_allreduce_ms": round(blk, 4),
+               "bucket_bytes": self._bucket_bytes, "collectives_per_step": self._n_coll,
+               "world": self.world}
+        self._marks = []
+        return out
+
+    def _ar_timed(self, t, blk):
+        a = self._mark()
+        self._ar(t)
+        b = self._mark()
+        if a is not None:
+            blk.append((a, b))
 
     def _ar(self, t):
         if self.coll:
@@ -95,28 +148,42 @@ class DataParallelStep:
 
     def step(self, x, areas, eps=None):
         e = self.e
+        blk = []
         e.forward(x, eps)
         if self.cosine:
-            self._ar(e.colsq)
+            self._ar_timed(e.colsq, blk)
         e.metric(areas)
         # the 5 loss sums are final after metric(): reduce them beside the backward
         h_loss = None
         if self.reduce_losses and self.coll:
             h_loss = dist.all_reduce(e.losses, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         if self.cosine:
-            self._ar(e.coldot)
+            self._ar_timed(e.coldot, blk)
         if self.coll and self.overlap:
             handles = []
+            nbytes = 0
             for part in range(e.N_BACKWARD_PARTS):
                 e.backward_part(part)
                 for view in e.grad_ranges(part):
                     handles.append(dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group,
                                                    async_op=True))
+                    nbytes += view.numel() * view.element_size()
+            w0 = self._mark()
             for h in handles:
                 h.wait()
+            w1 = self._mark()
+            if w0 is not None:
+                self._marks.append((blk, (w0, w1)))
+                self._bucket_bytes, self._n_coll = nbytes, len(handles) + len(blk) + (h_loss is not None)
         else:
             e.backward()
+            w0 = self._mark()
             self._ar(e.grads)
+            w1 = self._mark()
+            if w0 is not None and self.coll:
+                self._marks.append((blk, (w0, w1)))
+                self._bucket_bytes = e.grads.numel() * e.grads.element_size()
+                self._n_coll = 1 + len(blk) + (h_loss is not None)
         e.adam()
         if h_loss is not None:
             h_loss.wait()

@@ -44,3 +44,12 @@ def test_bench_self_launches_two_ranks_and_matches_one():
                       "loss_roofline"):
                 assert k in c, (cid, k)
     assert two["configs"]["C4"]["global_batch"] == 2 * two["configs"]["C4"]["per_gpu_batch"]
+    # communication figures with N ranks (none with one): exposed all-reduce wait per step, the
+    # bucket, and the bucket-sized all-reduce's bus bandwidth
+    assert one["comm"] is None
+    for c in (two["comm"], two["configs"]["C4"]["comm"], two["configs"]["C5"]["comm"]):
+        for k in ("exposed_allreduce_wait_ms", "blocking_stats_allreduce_ms", "bucket_bytes",
+                  "collectives_per_step", "allreduce_bench"):
+            assert k in c, k
+        assert c["bucket_bytes"] > 0 and c["steps"] == 3 and c["world"] == 2
+        assert c["allreduce_bench"]["busbw_GBps"] > 0

@@ -16,7 +16,7 @@ from tests.gpu_helpers import make_inputs, make_params, max_rel
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, metric, q, conv=False, size=24, chunks=4, cfg=None, early=False):
+def _worker(rank, world, port, metric, q, conv=False, size=24, chunks=4, cfg=None, early=False, comm=False):
     import torch.distributed as dist
     from magic_amd.engine import Engine
     from magic_amd.parallel import DataParallelStep
@@ -32,19 +32,21 @@ def _worker(rank, world, port, metric, q, conv=False, size=24, chunks=4, cfg=Non
     if early:  # an engine left with Adam-on-the-side-stream on (e.g. by a collective-free step)
         eng.set_option("early_adam", 1)
     st = DataParallelStep(eng, wgrad0_chunks=chunks)
+    st.comm_timing = comm  # HIP-event timing of the collective waits (bench.py's comm block)
     if chunks > 1:
         assert eng.N_BACKWARD_PARTS > 3  # the layer-0 weight gradient really runs in row chunks
     st.step(torch.from_numpy(X[sl]).cuda(), torch.from_numpy(areas[sl]).cuda(),
             torch.from_numpy(np.ascontiguousarray(eps[:, sl])).cuda())
     torch.cuda.synchronize()
     q.put((rank, eng.grads.cpu().numpy(), eng.losses.cpu().numpy(),
-           {k: v.cpu().numpy() for k, v in eng.params().items()}))
+           {k: v.cpu().numpy() for k, v in eng.params().items()}, st.comm_stats() if comm else None))
     eng.close()
     dist.destroy_process_group()
 
 
-def _dp2(cfg, metric="cosine", chunks=4, early=False):
-    """2 spawned gloo ranks on this GPU, each half of cfg.batch: {rank: (grads, losses, params)}"""
+def _dp2(cfg, metric="cosine", chunks=4, early=False, comm=False):
+    """2 spawned gloo ranks on this GPU, each half of cfg.batch: {rank: (grads, losses, params,
+    comm_stats)}"""
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
@@ -52,10 +54,10 @@ def _dp2(cfg, metric="cosine", chunks=4, early=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, metric, q),
-                         kwargs=dict(chunks=chunks, cfg=cfg, early=early)) for r in range(2)]
+                         kwargs=dict(chunks=chunks, cfg=cfg, early=early, comm=comm)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r, (g, l, P)) for r, g, l, P in (q.get(timeout=600) for _ in range(2)))
+    res = dict((r, (g, l, P, c)) for r, g, l, P, c in (q.get(timeout=600) for _ in range(2)))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -107,11 +109,36 @@ def test_dp2_c4_per_rank_shape_matches_full_batch():
     g_ref, l_ref, _ = _single(cfg)
     res = _dp2(cfg, chunks=4)
     for r in range(2):
-        g, l, _ = res[r]
+        g, l, _, _ = res[r]
         np.testing.assert_allclose(l, l_ref, rtol=2e-3)
         err = max_rel(g, g_ref)
         print(f"C4 per-rank shape, rank {r}: losses {l.tolist()} vs {l_ref.tolist()}; bucket max-rel {err:.3e}")
         assert err <= 5e-2, err
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+
+
+def test_dp2_c5_per_rank_shape_matches_full_batch():
+    """BASELINE C5's per-rank workload (8e: L = 2000, reciprocal squared-difference metric -- no
+    mid-step statistics collective -- bf16, B = 8192 per rank) through DataParallelStep: 2 gloo
+    ranks on this GPU against one process on the concatenated 16 384-pair batch, losses and the
+    whole all-reduced bucket at the bf16 bar; the collectives timed with HIP events as bench.py's
+    comm block does (the exposed all-reduce wait, the bucket: the whole [g1 | g2] buffer)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from magic_amd.config import baseline_config
+    cfg = baseline_config("C5").replace(batch=16384)
+    assert cfg.latent == 2000 and cfg.reciprocal and cfg.metric == "sqdiff"
+    g_ref, l_ref, _ = _single(cfg)
+    res = _dp2(cfg, chunks=4, comm=True)
+    for r in range(2):
+        g, l, _, c = res[r]
+        np.testing.assert_allclose(l, l_ref, rtol=2e-3)
+        err = max_rel(g, g_ref)
+        print(f"C5 per-rank shape, rank {r}: losses {l.tolist()} vs {l_ref.tolist()}; bucket max-rel "
+              f"{err:.3e}; comm {c}")
+        assert err <= 5e-2, err
+        assert c["steps"] == 1 and c["bucket_bytes"] == g.nbytes and c["exposed_allreduce_wait_ms"] >= 0
+        assert c["blocking_stats_allreduce_ms"] == 0  # squared difference: no statistics collective
     np.testing.assert_array_equal(res[0][0], res[1][0])
 
 
@@ -144,7 +171,7 @@ def test_dp2_on_gpu_matches_full_batch(metric, conv, size, chunks):
     procs = [ctx.Process(target=_worker, args=(r, 2, port, metric, q, conv, size, chunks)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict((r, (g, l)) for r, g, l, _ in (q.get(timeout=300) for _ in range(2)))
+    res = dict((r, (g, l)) for r, g, l, _, _ in (q.get(timeout=300) for _ in range(2)))
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
