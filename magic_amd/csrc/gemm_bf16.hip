@@ -771,7 +771,6 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   p.diag = d.diag;
   p.stamps = d.stamps;
   p.abits = d.Abits; p.abits_kts = d.abits_kts; p.abits_sb = d.abits_sb; p.anb = d.anb;
-  p.bits_mode = d.bits_mode;
   // tile order: bands of 8 m-tiles walked n by n when a row has >= 8 n-tiles, so the 32 tiles
   // an XCD holds at once share 8 A and 4 B tiles in its L2 (C5 latent-head forward
   // 24576 x 4000 x 501: 0.177 -> 0.161 ms; neutral on the BCE head and the other shapes,

@@ -196,13 +196,10 @@ __device__ __forceinline__ void bits_expand(u32x2 w, bf16x8 (&fa)[8]) {
 // main-loop state of one workgroup (registers once inlined). ST: stamped diagnostics build --
 // per wave the k-loop's shader-clock cycles and, with diag 16, each of a k-tile's 8
 // barrier-delimited slots summed over the k-loop (mvae_bench_gemm with MVAE_STAMPS=2; never in
-// the step). BM: A from a BitMat -- 1 expanded in registers per wave (the plane path's A images,
-// reads and DMA unused), 2 expanded once per workgroup into the plane path's A images (its
-// fragment reads and image-reusing walk unchanged; the DMA of A replaced by a 2 KB bits block per
-// k-tile, one ds_read_b32, 17 VALU and two ds_write_b128 per thread and half image)
-template <bool AT, bool BT, bool ST = false, int BM = 0>
+// the step). BITS: A from a BitMat, its fragments expanded in registers per wave (the plane
+// path's A images, reads and DMA unused)
+template <bool AT, bool BT, bool ST = false, bool BITS = false>
 struct E8 {
-  static constexpr bool BITS = BM == 1, BITW = BM == 2;
   static constexpr bool KA = !AT, KB = BT;  // operand images k-contiguous?
   HLoad<KA> la;
   HLoad<KB> lb;
@@ -225,37 +222,6 @@ struct E8 {
   const unsigned* Ab;
   unsigned bA;
   u32x2 wb0, wb1;
-  // BITW: LDS byte address of the bits ring (4 slots of 2 KB past the images: iteration u's block
-  // in slot u % 4) plus this thread's word offset in a half; its two chunks' byte offsets in a
-  // half image (the plane path's k-contiguous layout); lds0
-  unsigned rw, cofs[2], l0;
-  int hsel;
-  unsigned wnext;  // BITW: the word of the next tile's A1 (read one phase ahead)
-
-  // BITW: the 2 KB block of k-tile kt into ring slot `slot`, 256 B per wave
-  __device__ __forceinline__ void issue_ring(const Tile& t, int kt, int slot) {
-    typedef __attribute__((address_space(3))) void* lds_ptr;
-    const unsigned* src = Ab + (size_t)(t.ks / EBK + kt) * BITMAT_BLOCK_WORDS + wave * 64 + (threadIdx.x & 63);
-    __builtin_amdgcn_global_load_lds(src, (lds_ptr)(reinterpret_cast<char*>(smem) + 8 * EHB + slot * 2048 + wave * 256),
-                                     4, 0, 0);
-  }
-  // BITW: this thread's word of half H of ring slot `slot` (asm: the caller waits lgkmcnt)
-  __device__ __forceinline__ unsigned rd_word(int slot, int H) {
-    unsigned v;
-    asm volatile("ds_read_b32 %0, %1" : "=v"(v) : "v"(rw + (unsigned)(slot * 2048 + H * 1024)));
-    return v;
-  }
-  // BITW: expand word w into this thread's two chunks of half image (H, Bf)
-  template <int H, int Bf>
-  __device__ __forceinline__ void write_a(unsigned w) {
-    const unsigned sw = hsel ? w >> 8 : w;
-    const bf16x8 f0 = bits_frag(sw, 0), f1 = bits_frag(sw, 1);
-    typedef short s16x8_ __attribute__((ext_vector_type(8)));
-    const unsigned base = l0 + (unsigned)((2 * H + Bf) * EHB);
-    asm volatile("ds_write_b128 %0, %1" :: "v"(base + cofs[0]), "v"(__builtin_bit_cast(s16x8_, f0)) : "memory");
-    asm volatile("ds_write_b128 %0, %1" :: "v"(base + cofs[1]), "v"(__builtin_bit_cast(s16x8_, f1)) : "memory");
-  }
-
   // BITS: the 2 KB block of k-tile kt into bits buffer Bf, 256 B per wave
   template <int Bf>
   __device__ __forceinline__ void issue_bits(const Tile& t, int kt) {
@@ -347,56 +313,15 @@ struct E8 {
   // k-tile `it` (its images in buffer Bf); (kt1, pr1), (kt2, pr2): (k-tile, pair) of it+1, it+2;
   // ka1: it+1's A image is the one its buffer holds (from it-1: not copied again), ka2 / kb2: it+2's
   // A / B images likewise (from it)
-  // BITW: kt3 / ka3 -- it+3's k-tile and whether its A image is reused (no bits block needed)
   template <int Bf>
   __device__ __forceinline__ void tile(const PParams& pp, const Tile& t, int it, int total, int kt1, int pr1,
-                                       int kt2, int pr2, bool ka1, bool ka2, bool kb2, int kt3 = 0,
-                                       bool ka3 = false) {
+                                       int kt2, int pr2, bool ka1, bool ka2, bool kb2) {
     constexpr int Bn = Bf ^ 1;
     // stamped builds' A/B switches (results meaningless): diag 1 = no DMA after the prologue,
     // 64 = no fragment reads
     const bool dma = !ST || !(pp.diag & 1), rdf = !ST || !(pp.diag & 64);
     const bool h1 = it + 1 < total && dma, h2 = it + 2 < total && dma;
     const bool ia2 = h2 && !ka2, ib2 = h2 && !kb2;
-    constexpr int NB = KB ? 4 : 8;  // B-sub fragment reads
-    if constexpr (BITW) {
-      // p1 (0,0): A1 of it+1 into the other buffer (whose last reads were tile it-1's p3) from the
-      // word read in tile it-1's p4; it+3's block into the ring; then the B-sub 0 reads retired
-      rd_b<0, Bf>(fb0);
-      rd_a<0, Bf>(fa0);
-      if (h1 && !ka1) write_a<1, Bn>(wnext);
-      if (it + 3 < total && !ka3) issue_ring(t, kt3, (it + 3) & 3);
-      if (h1 && !ka1) asm volatile("s_waitcnt lgkmcnt(10)" ::: "memory");
-      else asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-      sbar<0>();
-      mfma_q<0, 0>(fa0, fb0);
-      sbar<1>();
-      // p2 (0,1): the word of it+2's half 0 (its block landed by tile it-1's p4)
-      rd_b<1, Bf>(fb1);
-      unsigned w0 = ia2 ? rd_word((it + 2) & 3, 0) : 0u;
-      if (ib2) issue_b<0, Bf>(pp, t, kt2, pr2);
-      sbar<2>();
-      mfma_q<0, 1>(fa0, fb1);  // (its lgkmcnt(0) retires the word)
-      asm volatile("" : "+v"(w0));
-      sbar<3>();
-      // p3 (1,1): A0 of it+2 into this buffer (A-sub 0 read in p1, retired)
-      rd_a<1, Bf>(fa1);
-      if (ia2) write_a<0, Bf>(w0);
-      sbar<4>();
-      mfma_q<1, 1>(fa1, fb1);
-      sbar<5>();
-      // p4 (1,0): it+1 landed, and it+3's block (issued in p1, before the B halves of it+2); the
-      // word of it+2's half 1 for the next tile's p1
-      if (ia2) wnext = rd_word((it + 2) & 3, 1);
-      if (ib2) issue_b<1, Bf>(pp, t, kt2, pr2);
-      if (ib2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      sbar<6>();
-      mfma_q<1, 0>(fa1, fb0);
-      asm volatile("" : "+v"(wnext));
-      sbar<7>();
-      return;
-    }
     // p1 (0,0)
     if (rdf) rd_b<0, Bf>(fb0);
     __builtin_amdgcn_sched_barrier(0);
@@ -455,11 +380,10 @@ struct E8 {
   }
 };
 
-// One workgroup's tile: the k-loop and the epilogue. BM > 0: A from the BitMat pp.abits (its AT
-// is then immaterial: the bits paths have one A layout, k-contiguous)
-template <bool AT, bool BT, int EPI, bool TE, bool ST, int BM>
+// One workgroup's tile: the k-loop and the epilogue. BITS: A from the BitMat pp.abits (its AT
+// is then immaterial: the bits path has one A layout)
+template <bool AT, bool BT, int EPI, bool TE, bool ST, bool BITS>
 __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
-  constexpr bool BITS = BM == 1, BITW = BM == 2;
   const Params& p = pp.g;
   unsigned long long st_k0 = 0, st_k2 = 0;  // stamped builds: kernel start, k-loop end (realtime)
   if constexpr (ST) st_k0 = __builtin_amdgcn_s_memrealtime();
@@ -468,14 +392,14 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
   const int wm = wave >> 2, wn = wave & 3;
   const Tile t = tile_of_t<256, 256>(p, true);
 
-  using S = E8<AT, BT, ST, BM>;
+  using S = E8<AT, BT, ST, BITS>;
   S s;
   s.A = pp.A + t.bi * p.sA;
   s.Bm = pp.B + t.bi * p.sB;
   s.smem = smem;
   s.wave = __builtin_amdgcn_readfirstlane(wave);
   if constexpr (ST) s.st_slots = (pp.diag & 16) != 0;
-  if constexpr (BM > 0) {
+  if constexpr (BITS) {
     s.Ab = pp.abits + (size_t)t.bi * pp.abits_sb + (size_t)(t.m0 / 256) * pp.abits_kts * BITMAT_BLOCK_WORDS;
   } else {
     s.la.init(p.lda, t.m0, p.M, wave, lane);
@@ -494,20 +418,6 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
     s.bA = lds0 + (unsigned)(wm * 512 + lane * 8);  // quarter (0, wm): rows 64 wm .. of half 0
   } else if constexpr (S::KA) {
     s.aA[0] = lds0 + frag_addr<true>(64 * wm, lane);
-    if constexpr (BITW) {
-      // this thread: word wi = tid >> 1 of a half's 256 (quarter wm' = wi >> 7, lane' = (wi >> 1) &
-      // 63, j = wi & 1) and its fragment rows h = tid & 1: row i = 64 wm' + 16 (2 j + h) +
-      // (lane' & 15) of the half, k-group g = lane' >> 4, k-halves kh = 0, 1 -> the chunk (row i,
-      // k 32 kh + 8 g) of the k-contiguous image: subtile 2 (i >> 4) + kh, st_16x32-swizzled
-      const int wi = tid >> 1, lq = (wi >> 1) & 63;
-      const int i = 64 * (wi >> 7) + 16 * (2 * (wi & 1) + (tid & 1)) + (lq & 15), g = lq >> 4;
-#pragma unroll
-      for (int kh = 0; kh < 2; ++kh)
-        s.cofs[kh] = (unsigned)(((i >> 4) * 2 + kh) * 1024) + st_swz((unsigned)((i & 15) * 64 + g * 16));
-      s.rw = lds0 + 8 * EHB + (unsigned)(wi * 4);
-      s.l0 = lds0;
-      s.hsel = tid & 1;
-    }
   } else {
 #pragma unroll
     for (int mb = 0; mb < 4; ++mb) s.aA[mb] = lds0 + frag_addr<false>(64 * wm + 16 * mb, lane);
@@ -520,7 +430,7 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
   }
 
   // (bits: A is exact, its residual planes zero -- the pairs with A plane 0)
-  const int np = BM > 0 ? pp.npairs_a0 : (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
+  const int np = BITS ? pp.npairs_a0 : (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
   const int nkt = t.ks < t.ke ? (t.ke - t.ks + EBK - 1) / EBK : 0;
   const int total = np * nkt;
   // waves 4-7 (the second wave of every SIMD), as a scalar condition: s_barrier ignores EXEC
@@ -547,12 +457,11 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
     };
     auto pa_of = [&](int pr) { return (pp.pab >> (4 * pr)) & 3; };
     auto pb_of = [&](int pr) { return (pp.pab >> (4 * pr + 2)) & 3; };
-    // cursors of iterations it-1 .. it+3
-    Cur cm{0, 0, 0, 0}, c0{0, 0, 0, 0}, c1{0, 0, 0, 0}, c2{0, 0, 0, 0}, c3{0, 0, 0, 0};
+    // cursors of iterations it-1 .. it+2
+    Cur cm{0, 0, 0, 0}, c0{0, 0, 0, 0}, c1{0, 0, 0, 0}, c2{0, 0, 0, 0};
     set(c0);
     c1 = c0; adv(c1);
     c2 = c1; adv(c2);
-    c3 = c2; adv(c3);
     // iteration j's image (A or B) is already in its buffer: iteration j-2 had the same k-tile
     // and plane (it+1's A: from it-1 -- cm; it+2's: from it -- c0)
     auto ka = [&](const Cur& a, const Cur& b, int j) { return rw && j >= 2 && a.kt == b.kt && pa_of(a.pr) == pa_of(b.pr); };
@@ -560,37 +469,7 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
     // prologue: A0 B0 B1 A1 of k-tile 0, then B0 A0 B1 of k-tile 1 (its A1: tile 0's p1); the bits
     // path: k-tile 0's block, B0 B1, then k-tile 1's B0 B1 (its block: tile 0's p1)
     int kt1 = c1.kt, pr1 = c1.pr, kt2 = c2.kt, pr2 = c2.pr;
-    if constexpr (BITW) {
-      // the blocks of iterations 0, 1, 2 into ring slots 0-2, the B halves of 0 and 1; once the
-      // blocks landed (and every wave's, after a barrier), A0 A1 of iteration 0 and A0 of 1
-      const bool b2 = total > 2 && !ka(c2, c0, 2);
-      s.issue_ring(t, 0, 0);
-      if (total > 1) s.issue_ring(t, kt1, 1);
-      if (b2) s.issue_ring(t, kt2, 2);
-      s.template issue_b<0, 0>(pp, t, 0, 0);
-      s.template issue_b<1, 0>(pp, t, 0, 0);
-      if (total > 1) {
-        s.template issue_b<0, 1>(pp, t, kt1, pr1);
-        s.template issue_b<1, 1>(pp, t, kt1, pr1);
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      }
-      bar();
-      {
-        unsigned w00 = s.rd_word(0, 0), w01 = s.rd_word(0, 1);
-        unsigned w10 = total > 1 ? s.rd_word(1, 0) : 0u;
-        s.wnext = total > 1 ? s.rd_word(1, 1) : 0u;  // tile 0's p1: A1 of iteration 1
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        asm volatile("" : "+v"(w00), "+v"(w01), "+v"(w10), "+v"(s.wnext));
-        s.template write_a<0, 0>(w00);
-        s.template write_a<1, 0>(w01);
-        if (total > 1) s.template write_a<0, 1>(w10);
-      }
-      if (total > 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    } else if constexpr (BITS) {
+    if constexpr (BITS) {
       s.template issue_bits<0>(t, 0);
       s.template issue_b<0, 0>(pp, t, 0, 0);
       s.template issue_b<1, 0>(pp, t, 0, 0);
@@ -624,14 +503,14 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
       st_r0 = __builtin_amdgcn_s_memrealtime();
       st_t0 = s.st_last = __builtin_amdgcn_s_memtime();
     }
-    auto step = [&]() { cm = c0; c0 = c1; c1 = c2; c2 = c3; adv(c3); };
+    auto step = [&]() { cm = c0; c0 = c1; c1 = c2; adv(c2); };
     for (int it = 0; it < total; it += 2) {
       s.template tile<0>(pp, t, it, total, c1.kt, c1.pr, c2.kt, c2.pr, ka(c1, cm, it + 1), ka(c2, c0, it + 2),
-                         kb(c2, c0, it + 2), c3.kt, ka(c3, c1, it + 3));
+                         kb(c2, c0, it + 2));
       step();
       if (it + 1 < total) {
         s.template tile<1>(pp, t, it + 1, total, c1.kt, c1.pr, c2.kt, c2.pr, ka(c1, cm, it + 2),
-                           ka(c2, c0, it + 3), kb(c2, c0, it + 3), c3.kt, ka(c3, c1, it + 4));
+                           ka(c2, c0, it + 3), kb(c2, c0, it + 3));
         step();
       }
     }
@@ -702,12 +581,11 @@ __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
   // a 0/1 batch (the de-interleave's not-binary word, a uniform branch): A from its bits
   if constexpr (has_bits<BT, EPI, ST>) {
     if (pp.abits && (!pp.anb || *pp.anb == 0)) {
-      if (pp.bits_mode == 1) e8_tile<false, BT, EPI, TE, ST, 1>(pp, smem);
-      else e8_tile<false, BT, EPI, TE, ST, 2>(pp, smem);
+      e8_tile<false, BT, EPI, TE, ST, true>(pp, smem);
       return;
     }
   }
-  e8_tile<AT, BT, EPI, TE, ST, 0>(pp, smem);
+  e8_tile<AT, BT, EPI, TE, ST, false>(pp, smem);
 }
 
 template <bool AT, bool BT, int EPI, bool TE>

@@ -51,8 +51,6 @@ struct PParams {
   long long abits_sb = 0;
   const int* anb = nullptr;
   int npairs_a0 = 1;                // the leading pairs with A plane 0 (the bits path's pairs)
-  int bits_mode = 2;                // bits path: 1 fragments expanded in registers per wave, 2 the A
-                                    // images expanded once per workgroup (gemm_bf16e.hip E8)
 };
 
 // tanh as an odd [13/6] rational in x on [-7.905, 7.905] (clamped beyond, where tanh rounds to

@@ -1788,7 +1788,6 @@ extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int
     if (e == hipSuccess) e = hipMemsetAsync(pnb, 0, 16, st);
     if (e == hipSuccess) e = launch_bits_from_plane(d.Ap, lda, at != 0, M, K, (unsigned*)pbits, kts, (int*)pnb, st);
     d.Abits = (const unsigned*)pbits; d.abits_kts = kts; d.anb = (const int*)pnb;
-    if ((epi >> 15) & 1) d.bits_mode = 1;  // epi bit 15: fragments expanded per wave
   }
   // epi bit 12 (plane modes): the output as bf16 planes only (no fp32 store), as the step's
   // producers write their operand images; C then receives the planes' sum (host side)
@@ -2004,7 +2003,6 @@ extern "C" int mvae_bench_gemm(int M, int N, int K, int at, int bt, int batch, i
       for (int b = 0; e == hipSuccess && b < batch; ++b)
         e = launch_bits_from_plane(A_.p + (size_t)b * sa, lda, at != 0, M, K, bits + b * bw, kts, bnb + 2, st);
       d.Abits = bits; d.abits_kts = kts; d.abits_sb = (long long)bw; d.anb = bnb + 2;
-      if ((variant >> 22) & 1) d.bits_mode = 1;  // bit 22: fragments expanded per wave
     }
   }
   // epilogue (variant >> 8): the step's fused epilogues with their operand reads and the

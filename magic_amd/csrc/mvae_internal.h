@@ -100,7 +100,6 @@ struct GemmDesc {
   int abits_kts = 0;
   long long abits_sb = 0;
   const int* anb = nullptr;
-  int bits_mode = 2;                   // 1: fragments expanded per wave, 2: A images per workgroup
   GemmEpi epi;
 };
 

@@ -25,17 +25,15 @@ def _gemm(lib, M, N, K, A, at, Bm, ldc, flags, act=0):
     return C
 
 
-@pytest.mark.parametrize("mode", [2, 1], ids=["images", "frags"])
 @pytest.mark.parametrize("prec", [2, 1], ids=["f32x", "bf16"])
 @pytest.mark.parametrize("at", [0, 1], ids=["fwd", "wgrad"])
 @pytest.mark.parametrize("epi", [0, 1], ids=["store", "act"])
 @pytest.mark.parametrize("M,N,K", [(600, 520, 300), (256, 256, 64), (130, 257, 1001), (300, 500, 4099),
                                    (700, 260, 10001)])
-def test_gemm_bits_path_bitwise_equal_planes(mode, prec, at, epi, M, N, K):
+def test_gemm_bits_path_bitwise_equal_planes(prec, at, epi, M, N, K):
     """variant 13 forces the eight-phase kernel; epi bit 14 hands it A as a BitMat too: the bits
     path must reproduce the plane path bit for bit (ragged M / N / K, partial k-tiles, split-K at
-    K 4099 / 10001, one-block shapes), in both of its forms (A images expanded once per workgroup;
-    fragments expanded per wave, epi bit 15)."""
+    K 4099 / 10001, one-block shapes)."""
     lib = _lib.load()
     g = torch.Generator(device="cuda").manual_seed(M * 3 + N * 7 + K + 11 * at + epi)
     A = _bin(K, M, g) if at else _bin(M, K, g)
@@ -43,7 +41,7 @@ def test_gemm_bits_path_bitwise_equal_planes(mode, prec, at, epi, M, N, K):
     ldc = (N + 7) // 8 * 8
     flags = epi | (prec << 4) | (13 << 8)
     Cp = _gemm(lib, M, N, K, A, at, Bm, ldc, flags)
-    Cb = _gemm(lib, M, N, K, A, at, Bm, ldc, flags | (1 << 14) | ((mode == 1) << 15))
+    Cb = _gemm(lib, M, N, K, A, at, Bm, ldc, flags | (1 << 14))
     assert torch.equal(Cb[:, :N], Cp[:, :N])
     Ad = A[:, :M].double().T if at else A[:, :K].double()
     acc = Ad @ Bm[:, :N].double()

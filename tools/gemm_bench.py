@@ -72,8 +72,6 @@ def main():
             v, f = v[:-1], 1 << 20
         elif v.endswith("B"):
             v, f = v[:-1], 3 << 20
-        elif v.endswith("R"):  # bits, fragments expanded per wave
-            v, f = v[:-1], 7 << 20
         return int(v) | f
     variants = [(vparse(v), int(d)) for v in args.variants.split(",") for d in args.diag.split(",")]
     want = set(args.shapes.split(",")) if args.shapes else None
@@ -92,7 +90,7 @@ def main():
                 if rc != 0:
                     raise RuntimeError(lib.mvae_last_error(None))
                 res.setdefault((name, v), []).append(ms.value)
-    lab = [f"v{v & 0xfffff}" + {0: "", 1: "b", 3: "B", 7: "R"}[v >> 20] + (f"d{d}" if d else "") for v, d in variants]
+    lab = [f"v{v & 0xfffff}" + {0: "", 1: "b", 3: "B"}[v >> 20] + (f"d{d}" if d else "") for v, d in variants]
     print(f"{'shape':16s} {'MxNxK':>22s} batch " + " ".join(f"{x + ' TF/s':>12s}" for x in lab))
     for name, M, N, K, at, bt, batch, epi in sh:
         fl = 2.0 * M * N * K * batch
