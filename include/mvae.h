@@ -129,7 +129,10 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out);
  * conv2_half (0/1), conv2_nw (4/8/16), conv2_tpb (1/2), conv2_fpw (2/4), conv2_wg (4/8),
  * conv2_nchunk (> 0), enc_chain (0/1: bf16 mode, the encoder's hidden layers in one launch,
  * default 1), enc_chain_rows (its rows per workgroup, 16..96; 0 auto; both chains), dec_chain
- * (0/1: bf16 mode, the decoder's two hidden layers in one launch, default 1). Diagnostics, results
+ * (0/1: bf16 mode, the decoder's two hidden layers in one launch, default 1), bits (0/1: bf16 and
+ * f32x modes, the layer-0 pixel operand of a 0/1 batch as one bit per pixel -- the de-interleave
+ * writes BitMats instead of the bf16 plane and the eight-phase kernel expands the A fragments in
+ * registers; a batch with another pixel value takes the planes; default 1). Diagnostics, results
  * meaningless: diag_skip_deint (1: de-interleave only the first batch -- a timing bound),
  * diag_shadow_deint (-1 or a workgroup count > 0: a second de-interleave of each step's input
  * into a scratch image on a low-priority stream, launched at diag_shadow_at = 0 the forward,

@@ -313,9 +313,11 @@ struct E8 {
   // k-tile `it` (its images in buffer Bf); (kt1, pr1), (kt2, pr2): (k-tile, pair) of it+1, it+2;
   // ka1: it+1's A image is the one its buffer holds (from it-1: not copied again), ka2 / kb2: it+2's
   // A / B images likewise (from it)
+  // BITS: ka1 = it+1 has this iteration's k-tile (no block copy), ex = this iteration's k-tile differs
+  // from it-1's (expand; else the fragments in fa0 / fa1 are still this k-tile's)
   template <int Bf>
   __device__ __forceinline__ void tile(const PParams& pp, const Tile& t, int it, int total, int kt1, int pr1,
-                                       int kt2, int pr2, bool ka1, bool ka2, bool kb2) {
+                                       int kt2, int pr2, bool ka1, bool ka2, bool kb2, bool ex = true) {
     constexpr int Bn = Bf ^ 1;
     // stamped builds' A/B switches (results meaningless): diag 1 = no DMA after the prologue,
     // 64 = no fragment reads
@@ -329,12 +331,14 @@ struct E8 {
       // both quarters' words (the buffer is next restaged in tile it+1's p1); the whole block of
       // it+1 into the other buffer, whose last reads were tile it-1's p1; quarter 0 expanded once
       // every read retired (B-sub 0's as well: B0 is restaged in p2)
-      rd_bits<Bf>();
+      if (ex) rd_bits<Bf>();
       if (h1 && !ka1) issue_bits<Bn>(t, kt1);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      asm volatile("" : "+v"(wb0), "+v"(wb1));
-      __builtin_amdgcn_sched_barrier(0);
-      bits_expand(wb0, fa0);
+      if (ex) {
+        asm volatile("" : "+v"(wb0), "+v"(wb1));
+        __builtin_amdgcn_sched_barrier(0);
+        bits_expand(wb0, fa0);
+      }
     } else {
       if (rdf) rd_a<0, Bf>(fa0);
       if (h1 && !ka1) issue_a<1, Bn>(pp, t, kt1, pr1);
@@ -354,7 +358,7 @@ struct E8 {
     sbar<3>();
     // p3 (1,1)
     if constexpr (BITS) {
-      bits_expand(wb1, fa1);
+      if (ex) bits_expand(wb1, fa1);
     } else {
       if (rdf) rd_a<1, Bf>(fa1);
       if (ia2) issue_a<0, Bf>(pp, t, kt2, pr2);
@@ -444,7 +448,8 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
     // not copied again (binary pixels, 3 pairs: 2 of 6 A images copied; 6 pairs: 16 of 24
     // images). Cursor = (group g of two k-tiles, index r within it).
     struct Cur { int g, r, kt, pr; };
-    const bool rw = pp.reuse != 0;
+    // (the bits path walks pairs innermost: the pairs of a k-tile reuse its expanded fragments)
+    const bool rw = pp.reuse != 0 && !BITS;
     auto set = [&](Cur& c) {
       if (!rw) { c.kt = c.g; c.pr = c.r; return; }
       if (2 * c.g + 1 < nkt) { c.kt = 2 * c.g + (c.r & 1); c.pr = c.r >> 1; }
@@ -504,13 +509,17 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
       st_t0 = s.st_last = __builtin_amdgcn_s_memtime();
     }
     auto step = [&]() { cm = c0; c0 = c1; c1 = c2; adv(c2); };
+    // the bits path: it+1's block is copied only for a new k-tile, and an iteration expands only
+    // when its k-tile is not it-1's
+    auto ka1_of = [&](int j) { return BITS ? c1.kt == c0.kt : ka(c1, cm, j); };
+    auto ex_of = [&](int j) { return !BITS || j == 0 || c0.kt != cm.kt; };
     for (int it = 0; it < total; it += 2) {
-      s.template tile<0>(pp, t, it, total, c1.kt, c1.pr, c2.kt, c2.pr, ka(c1, cm, it + 1), ka(c2, c0, it + 2),
-                         kb(c2, c0, it + 2));
+      s.template tile<0>(pp, t, it, total, c1.kt, c1.pr, c2.kt, c2.pr, ka1_of(it + 1), ka(c2, c0, it + 2),
+                         kb(c2, c0, it + 2), ex_of(it));
       step();
       if (it + 1 < total) {
-        s.template tile<1>(pp, t, it + 1, total, c1.kt, c1.pr, c2.kt, c2.pr, ka(c1, cm, it + 2),
-                           ka(c2, c0, it + 3), kb(c2, c0, it + 3));
+        s.template tile<1>(pp, t, it + 1, total, c1.kt, c1.pr, c2.kt, c2.pr, ka1_of(it + 2),
+                           ka(c2, c0, it + 3), kb(c2, c0, it + 3), ex_of(it + 1));
         step();
       }
     }

@@ -448,8 +448,7 @@ struct CreateOpts {
   int enc_chain_rows = 0;  // ... its rows per workgroup forced (16..96, multiple of 16; 0 auto)
   int diag_chain = 0;      // ... its timing ablations (ChainArgs::diag; results meaningless)
   int dec_chain = 1;    // bf16 mode: the decoder's two hidden layers in one launch (0: one GEMM each)
-  int bits = 1;         // the layer-0 pixel operand of a 0/1 batch as bits (BitMat): 1 in bf16 mode,
-                        // 2 in the f32x mode too, 0 never
+  int bits = 1;         // plane modes: the layer-0 pixel operand of a 0/1 batch as bits (BitMat)
   int conv2_nw = 8, conv2_tpb = 1, conv2_fpw = 2, conv2_wg = 8, conv2_half = 1, conv2_nchunk = 0;
 };
 
@@ -482,7 +481,7 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "enc_chain" && in(0, 1)) o->enc_chain = (int)v;
     else if (k == "diag_chain" && in(0, 7)) o->diag_chain = (int)v;
     else if (k == "dec_chain" && in(0, 1)) o->dec_chain = (int)v;
-    else if (k == "bits" && in(0, 2)) o->bits = (int)v;
+    else if (k == "bits" && in(0, 1)) o->bits = (int)v;
     else if (k == "enc_chain_rows" && (v == 0 || (in(16, 96) && v % 16 == 0))) o->enc_chain_rows = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
     else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
@@ -827,8 +826,7 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
     GemmDesc& f0 = c->fwd_enc[0];
     GemmDesc& w0 = c->bwd_enc[c->nenc];
     auto planek = [](const GemmDesc& d) { return d.prec != GEMM_F32 && !d.valu && gemm_bf16_wide(d); };
-    // (bf16 mode: in f32x the bits path expands A once per plane pair and measured slower, r6b)
-    if (opt.bits && (c->np == 1 || (opt.bits == 2 && c->np)) && !c->conv && c->xbits && c->B % 64 == 0 && c->x32mask == 0 && planek(f0) &&
+    if (opt.bits && c->np && !c->conv && c->xbits && c->B % 64 == 0 && c->x32mask == 0 && planek(f0) &&
         planek(w0) && f0.A == c->xs && w0.A == c->xs) {
       c->kts_f = bitmat_kts(c->D + 1);
       c->kts_w = bitmat_kts(3 * c->B);
