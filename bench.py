@@ -75,6 +75,9 @@ def parse_args(argv=None):
                     help="libmvae schedule switch NAME=VALUE (mvae_set_option), repeatable")
     ap.add_argument("--create-opt", action="append", default=[],
                     help="libmvae plan-time kernel switch NAME=VALUE (mvae_create_ex), repeatable")
+    ap.add_argument("--mark-dominant", action="store_true",
+                    help="profiler runs: marker kernels around the dominant GEMM region's launches in "
+                         "the timed loop, so a kernel trace attributes them (tools/timed_steps.py)")
     ap.add_argument("--no-configs", action="store_true",
                     help="skip the configs block (C3 / C5 on one GPU; C4 / C5 with N ranks)")
     ap.add_argument("--no-h2d", action="store_true", help="skip the PCIe-inclusive h2d leg")
@@ -616,6 +619,8 @@ def measure(args, cfg, world, rank, local, dev, *, timing, steps, warmup, keep=F
         eng.timing_reset()
         eng.timing_select(dom)
         eng.timing_enable(True)
+        if args.mark_dominant:
+            eng.timing_marker(dom, True)
 
     host_t = []
 
@@ -641,6 +646,8 @@ def measure(args, cfg, world, rank, local, dev, *, timing, steps, warmup, keep=F
     stepper.comm_timing = world > 1  # exposed collective waits of the timed steps
     elapsed = timed(steps, lambda i: pool[i % 2])
     stepper.comm_timing = False
+    if timing and args.mark_dominant:
+        eng.timing_marker(dom, False)
     comm = None
     if world > 1:
         comm = stepper.comm_stats()

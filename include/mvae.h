@@ -191,7 +191,7 @@ int mvae_grad_range(mvae_ctx* ctx, int part, int index, float** ptr, size_t* cou
  * backward has written their gradients (beside the layer-0 weight gradient): only for callers
  * that neither read nor modify MVAE_BUF_GRADS between mvae_backward and mvae_adam (no
  * all-reduce): the caller's stream then joins the side stream in mvae_adam;
- * mvae_train_step uses it in the bf16 and f32x modes; "early_chunks" (1, 2, 4, 8; default 2):
+ * mvae_train_step uses it in the bf16 and f32x modes; "early_chunks" (1, 2, 4, 8; default 1):
  * with the early Adam and "wgrad0_chunks" 1, mvae_backward runs the layer-0 weight gradient in
  * that many row chunks and updates each chunk's parameter rows but the last's on the side stream
  * beside the next chunk's GEMM, i.e. already inside mvae_backward (so with early_adam the

@@ -109,8 +109,9 @@ struct mvae_ctx {
   // side stream beside chunk k + 1's GEMM: mvae_adam's layer-0 launch starts here
   size_t adam0_from = 0;
   // the single-call backward with the early Adam runs the layer-0 weight gradient in this many
-  // chunks when "wgrad0_chunks" is 1 (option "early_chunks"; 1: one GEMM)
-  int early_chunks = 2;
+  // chunks when "wgrad0_chunks" is 1 (option "early_chunks"; 1: one GEMM, the default since the
+  // chunks keep the one-GEMM plan: 1 vs 2 chunks C2 -2.5 %, C3 -2.4 %, C5 -1.0 %, r6l)
+  int early_chunks = 1;
   int side_mask = 3;         // option "side_mask": weight gradients on the side stream -- bit 0
                              // the decoder's, bit 1 the encoder's (else in order on the caller's)
   bool valu = true;          // skinny GEMMs on the fp32 VALU kernel (env MVAE_NO_VALU=1: off)
@@ -1530,8 +1531,9 @@ extern "C" int mvae_backward_part(mvae_ctx* ctx, int part, void* stream) {
 extern "C" int mvae_backward(mvae_ctx* ctx, void* stream) {
   if (!ctx) return MVAE_EINVAL;
   if (ctx->phase != 2) return fail(ctx, MVAE_ESTATE, "mvae_backward before mvae_metric");
-  // early Adam: the layer-0 weight gradient in early_chunks chunks, Adam of each chunk but the last
-  // beside the next chunk's GEMM (C2 -0.003, C3 -0.003, C5 -0.034 ms at 2 chunks, r5zw)
+  // early Adam: the layer-0 weight gradient in early_chunks chunks (default 1), Adam of each chunk
+  // but the last beside the next chunk's GEMM (r5zw: -0.003 to -0.034 ms at 2 chunks with the
+  // chunks' own plans; with the one-GEMM plan pinned, 2 chunks cost +1-2.5 %, r6l)
   const int w0 = ctx->w0_chunks;
   if (ctx->early_adam && ctx->use_side && ctx->side && w0 == 1 && ctx->early_chunks > 1 && !ctx->conv &&
       ctx->enc[0].off == 0)

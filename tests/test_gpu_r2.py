@@ -312,7 +312,7 @@ def test_early_adam_is_bitwise_identical(prec):
     """Option early_adam (Adam of the blocks after layer 0 on the side stream, beside the layer-0
     weight gradient) vs one Adam launch after the backward, and mvae_train_step (which uses it
     in the plane modes), with the layer-0 weight gradient as one GEMM or in two row chunks (chunk
-    0's rows updated beside chunk 1's GEMM, the default of the early Adam: option early_chunks):
+    0's rows updated beside chunk 1's GEMM: option early_chunks):
     all bitwise identical parameters after three steps."""
     cfg = preset("8c", image_size=40, batch=768, precision=prec).replace(enc=(400, 300, 260))
     P = make_params(cfg)
@@ -323,11 +323,11 @@ def test_early_adam_is_bitwise_identical(prec):
         eng = _engine(cfg)  # fresh Adam state per mode
         try:
             eng.set_option("early_adam", 1 if mode.startswith("early") else 0)
-            if mode == "train_step2":  # the default: two chunks under the early Adam
-                pass
+            if mode == "train_step2":  # two chunks under the early Adam
+                eng.set_option("early_chunks", 2)
             elif mode.endswith("2"):  # layer-0 weight gradient in two chunks: chunk 0's Adam early
                 eng.set_option("wgrad0_chunks", 2)
-            else:  # one layer-0 GEMM, also with the early Adam (default: early_chunks = 2)
+            else:  # one layer-0 GEMM, also with the early Adam (the default: early_chunks = 1)
                 eng.set_option("early_chunks", 1)
             eng.load_params(P)
             for _ in range(3):

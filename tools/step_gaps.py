@@ -5,13 +5,15 @@ covers), with the five largest gaps and where the next step starts. The timed lo
 the ones with idle time of a few tens of us (the region pass serialises its launches behind
 event records). usage: python tools/step_gaps.py <kernel_trace.csv>"""
 import csv
+import re
 import sys
 
 
 def main():
     rows = [r for r in csv.DictReader(open(sys.argv[1])) if "mvae::" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    ad = [i for i, r in enumerate(rows) if "deinterleave" in r["Kernel_Name"]]
+    # a step starts at the de-interleave (the bits form, or the plane form; not the gated grey pass)
+    ad = [i for i, r in enumerate(rows) if re.search(r"::(deint_bits|deinterleave_vec)", r["Kernel_Name"])]
     for k in range(1, len(ad)):
         seg = rows[ad[k - 1]:ad[k]]
         iv = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in seg)

@@ -11,7 +11,8 @@ import sys
 def main():
     rows = [r for r in csv.DictReader(open(sys.argv[1])) if "mvae::" in r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    ad = [i for i, r in enumerate(rows) if "deinterleave" in r["Kernel_Name"]]
+    # a step starts at the de-interleave (the bits form, or the plane form; not the gated grey pass)
+    ad = [i for i, r in enumerate(rows) if re.search(r"::(deint_bits|deinterleave_vec)", r["Kernel_Name"])]
     best = None
     for k in range(1, len(ad)):
         seg = rows[ad[k - 1]:ad[k]]
