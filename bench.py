@@ -153,6 +153,13 @@ def plane_pairs(cfg, name: str, exact_pixels: bool) -> int:
     return 3 if name in ("enc_fwd_0", "enc_bwd_w_0") and exact_pixels else 6
 
 
+def bits_on(cfg) -> bool:
+    """The library's bits path for the layer-0 pixel operand (create option bits, default on):
+    plane modes, FC encoder, 64-row batch blocks, whole 8-pixel groups."""
+    return (cfg.precision in ("bf16", "f32x") and not cfg.conv and cfg.batch % 64 == 0
+            and cfg.D % 8 == 0 and "bits=0" not in (getattr(cfg, "options", "") or ""))
+
+
 def region_bytes(cfg, name: str) -> float:
     """Algorithmic HBM bytes per launch of a bandwidth-bound region: every operand read once and
     every output written once at its stored width (fp32 = 4 B; bf16 plane images = 2 B per plane,
@@ -163,6 +170,8 @@ def region_bytes(cfg, name: str) -> float:
     np_ = {"f32": 0, "bf16": 1, "f32x": 3}[cfg.precision]
     BL = B * L
     if name == "deinterleave":  # fp32 X read; bf16 plane 0 of 3 blocks (plane modes) or fp32 xs
+        if bits_on(cfg):  # ... or the two BitMats (3 bits per pixel each) and the target's bits
+            return B * D * (12.0 + 7.0 / 8.0)
         return B * D * (12.0 + (6.0 if np_ else 12.0))
     if name == "eps_rng":       # caller-given eps copied once (internal draws: no kernel)
         return 3 * BL * 8.0
@@ -863,7 +872,7 @@ def run_plan(args) -> dict:
 
     N = args.gpus
     ids = [args.config] + ([] if args.no_configs else
-                           [c for c in (["C3", "C5"] if N == 1 else ["C4", "C5"])
+                           [c for c in (["C3", "C5", "C5CONV"] if N == 1 else ["C4", "C5"])
                             if c != args.config and not (c == "C4" and args.config == "C3")])
     out = {"n_gpus": N, "launcher": "torch.distributed.run, one process per GPU" if N > 1 else "one process",
            "backend": "nccl (RCCL over xGMI)" if N > 1 else None, "configs": {}}
@@ -972,7 +981,8 @@ def main():
     # per rank, global batch 8192 N) and C5 at N ranks
     extra = {}
     if not args.no_configs:
-        ids = ["C3", "C5"] if world == 1 else ["C4", "C5"]
+        # (one GPU: also C5CONV, BASELINE config 5's conv-encoder variant -- SURVEY.md §8 f4)
+        ids = ["C3", "C5", "C5CONV"] if world == 1 else ["C4", "C5"]
         for cid in ids:
             if cid == args.config or (cid == "C4" and args.config == "C3"):
                 continue

@@ -1045,7 +1045,8 @@ hipError_t launch_deint_bits(const float* x, int B, int D, unsigned* xbf, int kt
       hipLaunchKernelGGL((deint_bits_kernel<2, 256, 72>), dim3((kts_f + 1) / 2, B / 64), dim3(256), 0, st, x4, B, D,
                          kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
   }
-  hipLaunchKernelGGL(deint_grey_kernel, dim3(1024), dim3(256), 0, st, reinterpret_cast<const float4*>(x), xs,
+  // (256 workgroups striding: for a 0/1 batch every one returns at once, and fewer cost less)
+  hipLaunchKernelGGL(deint_grey_kernel, dim3(256), dim3(256), 0, st, reinterpret_cast<const float4*>(x), xs,
                      xp.p, xp.stride, xp.n, f32dyn_mask, dyn, B, D, ldx);
   return hipGetLastError();
 }

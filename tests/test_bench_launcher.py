@@ -35,9 +35,9 @@ def test_bench_self_launches_two_ranks_and_matches_one():
     for k in ("metric", "value", "unit", "steps", "warmup", "ms_per_step", "higher_is_better",
               "vs_baseline", "dtype", "data", "roofline", "cpu_baseline", "h2d", "configs", "build_id"):
         assert k in two and k in one
-    # the configs block: C3 / C5 on one GPU, C4 (C3's shape per rank) / C5 with N ranks, each
+    # the configs block: C3 / C5 / C5CONV on one GPU, C4 (C3's shape per rank) / C5 with N ranks, each
     # with its own value and rooflines
-    assert set(one["configs"]) == {"C3", "C5"} and set(two["configs"]) == {"C4", "C5"}
+    assert set(one["configs"]) == {"C3", "C5", "C5CONV"} and set(two["configs"]) == {"C4", "C5"}
     for line in (one, two):
         for cid, c in line["configs"].items():
             for k in ("workload", "value", "ms_per_step", "global_batch", "per_gpu_batch", "roofline",
