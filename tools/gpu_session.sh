@@ -1,8 +1,14 @@
 #!/bin/bash
 # The current GPU session (overwritten per session; earlier sessions are in git history):
 #   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r6m: timed-loop kernel traces with markers around the dominant region, C2 / C3 / C5 (defaults)
+# r6n: the round-6 tree -- whole GPU suite, smoke, per-config timed-loop kernel traces (markers
+# around the dominant region) and the default bench line (CPU baseline, PMC traffic, configs)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+T="python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider"
 B="--no-cpu-baseline --pmc off --no-h2d --no-pipeline --no-configs --steps 20 --warmup 3 --mark-dominant"
-p() { echo "r6m_prof_$1|240|cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/gpurun_out/prof_r6m_$1 -o run -- python3 $PWD/bench.py --config $2 $B"; }
-bash tools/gpu_steps.sh "$(p c2 C2)" "$(p c3 C3)" "$(p c5 C5)"
+p() { echo "r6n_prof_$1|240|cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/gpurun_out/prof_r6n_$1 -o run -- python3 $PWD/bench.py --config $2 $B"; }
+bash tools/gpu_steps.sh \
+  "r6n_tests|700|$T -m gpu tests" \
+  "r6n_smoke|240|python -c 'import __graft_entry__ as g; g.smoke()'" \
+  "$(p c2 C2)" "$(p c3 C3)" "$(p c5 C5)" \
+  "r6n_bench|900|python bench.py > gpurun_out/r6n_bench.json"
