@@ -50,7 +50,7 @@ METRIC = "shape-pairs/sec/GPU (train step) + overlap-MSE, 100×100 pairs, 1/2/4/
 F32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: v_mfma_f32_32x32x2_f32 (exact fp32)
 BF16_MFMA_PEAK_TFLOPS = 2500.0   # dense
 HBM_PEAK_GBS = 8000.0
-PMC_REGIONS_BW = ("deinterleave", "latent_bwd", "adam")
+PMC_REGIONS_BW = ("deinterleave", "deint_fwd0", "latent_bwd", "adam")
 # the layer-0 pair and the decoder-output trio: HBM traffic and the MFMA-busy fraction per region
 PMC_REGIONS_MFMA = ("enc_fwd_0", "enc_bwd_w_0", "dec_fwd_out_bce", "dec_bwd_d_out", "dec_bwd_w_out")
 
@@ -123,6 +123,8 @@ def region_flops(cfg, name: str) -> float:
             return 3 * B * conv2
         if name in ("conv2_dgrad", "conv2_wgrad"):
             return 4 * B * conv2
+    if name == "deint_fwd0":  # the de-interleave's workers inside the layer-0 forward's launch
+        name = "enc_fwd_0"
     if name == "enc_fwd_chain":  # the hidden layers 1 .. n-1 in one launch
         return sum(2.0 * 3 * B * widths[i] * widths[i + 1] for i in range(1, len(cfg.enc)))
     if name.startswith("enc_fwd_"):
@@ -798,6 +800,23 @@ def rooflines(args, m):
         loss_roofline[k] = {"bytes": by, "avg_ms": round(ms_k, 4),
                             "gbs": round(by / (ms_k * 1e-3) / 1e9, 1),
                             "frac": round(by / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+    if "deint_fwd0" in regions:
+        # the fused launch (create option deint_fuse): its bound is the larger of the
+        # de-interleave's HBM time and the forward's MFMA time at the dense peaks
+        ms_f = regions["deint_fwd0"][0] / args.region_steps
+        by_d = region_bytes(cfg, "deinterleave")
+        fl = region_flops(cfg, "enc_fwd_0") * (plane_pairs(cfg, "enc_fwd_0", m.get("dyn", 0) == 0)
+                                               if cfg.precision == "f32x" else 1)
+        t_hbm = by_d / (HBM_PEAK_GBS * 1e9)
+        t_mfma = fl / ((F32_MFMA_PEAK_TFLOPS if cfg.precision == "f32" else BF16_MFMA_PEAK_TFLOPS) * 1e12)
+        loss_roofline["deint_fwd0"] = {
+            "deint_bytes": by_d, "fwd_mfma_flops": fl, "avg_ms": round(ms_f, 4),
+            "hbm_bound_ms": round(t_hbm * 1e3, 4), "mfma_bound_ms": round(t_mfma * 1e3, 4),
+            "frac_of_bound": round(max(t_hbm, t_mfma) / (ms_f * 1e-3), 4),
+            "deint_gbs": round(by_d / (ms_f * 1e-3) / 1e9, 1),
+            "note": "the de-interleave's workers beside the layer-0 forward's tiles in one launch "
+                    "(DeintJob); bound = max(HBM time of the de-interleave's bytes, MFMA time of "
+                    "the forward's bf16 products)"}
     lat = [k for k in ("eps_rng", "latent_fwd", "colsq", "metric_loss", "coldot", "latent_bwd")
            if k in regions]
     ms_lat = sum(regions[k][0] / args.region_steps for k in lat)
@@ -849,8 +868,10 @@ def print_regions(args, m, tag):
     for k, (ms, n) in sorted(regions.items(), key=lambda kv: -kv[1][0]):
         fl = region_flops(cfg, k)
         extra = f"  {fl / (ms / rs * 1e-3) / 1e12:7.1f} TF/s" if fl else ""
-        if lr and k in lr:
+        if lr and k in lr and "gbs" in lr[k]:
             extra = f"  {lr[k]['gbs']:7.1f} GB/s"
+        elif lr and k in lr and "deint_gbs" in lr[k]:
+            extra = f"{extra}  {lr[k]['deint_gbs']:7.1f} GB/s of the de-interleave"
         print(f"[bench] {k:18s} {ms / rs:9.4f} ms/step ({n} launches){extra}", file=sys.stderr)
 
 

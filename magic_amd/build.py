@@ -22,7 +22,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("MVAE_ARCH", "gfx950")
 SOURCES = ["mvae_api.cpp", "gemm_f32.hip", "gemm_bf16.hip", "gemm_bf16e.hip", "gemm_valu.hip", "mvae_kernels.hip",
            "conv_tower.hip", "conv_mfma.hip", "enc_chain.hip"]
-HEADERS = ["mvae_internal.h", "gemm_common.h", os.path.join("..", "..", "include", "mvae.h")]
+HEADERS = ["mvae_internal.h", "gemm_common.h", "deint_bits.h", os.path.join("..", "..", "include", "mvae.h")]
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result",
           "-Wno-unused-value", "-I", os.path.join(ROOT, "include")]
 

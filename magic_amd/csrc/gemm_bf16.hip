@@ -771,6 +771,11 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   p.diag = d.diag;
   p.stamps = d.stamps;
   p.abits = d.Abits; p.abits_kts = d.abits_kts; p.abits_sb = d.abits_sb; p.anb = d.anb;
+  p.dj = d.dj;
+  p.bits_reg = d.bits_reg;
+  // the fused de-interleave rides on the eight-phase kernel's bits path only
+  if (d.dj.nworkers && (g.tn != TN_E8 || !d.Abits || d.at || d.bt || (epi != EPI_STORE && epi != EPI_ACT)))
+    return hipErrorInvalidValue;
   // tile order: bands of 8 m-tiles walked n by n when a row has >= 8 n-tiles, so the 32 tiles
   // an XCD holds at once share 8 A and 4 B tiles in its L2 (C5 latent-head forward
   // 24576 x 4000 x 501: 0.177 -> 0.161 ms; neutral on the BCE head and the other shapes,

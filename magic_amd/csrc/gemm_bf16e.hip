@@ -36,6 +36,7 @@
 //     conflict-free (the 16 lanes of a group: 4 k-rows x 4 row quads; the two groups of a
 //     32-lane half: k-rows 8 apart, slots XORed by 2).
 #include "gemm_common.h"
+#include "deint_bits.h"
 
 #include <cstdint>
 
@@ -197,8 +198,11 @@ __device__ __forceinline__ void bits_expand(u32x2 w, bf16x8 (&fa)[8]) {
 // per wave the k-loop's shader-clock cycles and, with diag 16, each of a k-tile's 8
 // barrier-delimited slots summed over the k-loop (mvae_bench_gemm with MVAE_STAMPS=2; never in
 // the step). BITS: A from a BitMat, its fragments expanded in registers per wave (the plane
-// path's A images, reads and DMA unused)
-template <bool AT, bool BT, bool ST = false, bool BITS = false>
+// path's A images, reads and DMA unused) -- 1: each k-tile's block copied into LDS by one
+// 256-B LDS-DMA per wave, each wave reading its two quarters from there; 2: each wave loads its
+// two quarters' words straight into registers (two 8-B `sc1` loads per lane), the form of the
+// fused de-interleave's consumers (DeintJob)
+template <bool AT, bool BT, bool ST = false, int BITS = 0>
 struct E8 {
   static constexpr bool KA = !AT, KB = BT;  // operand images k-contiguous?
   HLoad<KA> la;
@@ -222,6 +226,11 @@ struct E8 {
   const unsigned* Ab;
   unsigned bA;
   u32x2 wb0, wb1;
+  // BITS 2: the words of quarters 0 / 1 (each reloaded for the next k-tile right after its
+  // expansion: quarter 0 in p1, quarter 1 in p3), this lane's 8-B index in a block (quarter 0), and
+  // the chunks known finished by the fused de-interleave
+  u32x2 wn0, wn1;
+  int wq, ready;
   // BITS: the 2 KB block of k-tile kt into bits buffer Bf, 256 B per wave
   template <int Bf>
   __device__ __forceinline__ void issue_bits(const Tile& t, int kt) {
@@ -233,6 +242,44 @@ struct E8 {
   __device__ __forceinline__ void rd_bits() {
     wb0 = rd_b64<Bf * 2048>(bA);
     wb1 = rd_b64<Bf * 2048 + 1024>(bA);
+  }
+  // BITS 2: a fused launch's chunk c is finished (the workers' done[c] reached B / 64): one `sc1`
+  // poll of the next 64 chunks' counters per try (lane i: chunk c + i), so one poll that finds
+  // the workers ahead covers every chunk they finished
+  __device__ __forceinline__ void gate(const PParams& pp, int c) {
+    if (c < ready) return;
+    const int lane = threadIdx.x & 63;
+    const int R = pp.dj.B >> 6;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      const int ci = c + lane;
+      const int v = ci < pp.dj.nchunks ? __hip_atomic_load(pp.dj.done + ci, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                       : R;
+      const unsigned long long ok = __ballot(v >= R);
+      if (ok & 1ull) {
+        ready = c + (~ok ? __builtin_ctzll(~ok) : 64);
+        return;
+      }
+      // (bounded: a worker that never finished -- 0.5 s at the 100 MHz realtime clock -- raises
+      // the job's error word; the launch then ends with invalid results instead of hanging)
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 50000000ull) {
+        if (lane == 0) atomicOr(pp.dj.err, 1);
+        ready = 1 << 30;
+        return;
+      }
+      __builtin_amdgcn_s_sleep(8);  // (~0.2 us: 1536 pollers stay off the counters' L2 lines)
+    }
+  }
+  // BITS 2: k-tile kt's words of this wave's quarter Q into wn0 / wn1 by an 8-B `sc1` load in
+  // inline asm (invisible to hipcc's waitcnt pass, which otherwise drains every load at once: the
+  // p4 / p3 waits below retire it); a fused launch first waits until the chunk is finished
+  template <int Q>
+  __device__ __forceinline__ void load_bits(const PParams& pp, const Tile& t, int kt) {
+    const int gk = t.ks / EBK + kt;
+    if (Q == 0 && pp.dj.nworkers && !(pp.dj.diag & 1)) gate(pp, gk / DEINT_FUSE_PB);
+    const unsigned* q = Ab + (size_t)gk * BITMAT_BLOCK_WORDS + 2 * wq + 256 * Q;
+    if constexpr (Q == 0) asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(wn0) : "v"(q) : "memory");
+    else asm volatile("global_load_dwordx2 %0, %1, off sc1" : "=v"(wn1) : "v"(q) : "memory");
   }
 
   template <int K>
@@ -327,7 +374,17 @@ struct E8 {
     // p1 (0,0)
     if (rdf) rd_b<0, Bf>(fb0);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (BITS) {
+    if constexpr (BITS == 2) {
+      // quarter 0 of this k-tile (landed by the last p4's wait) expanded, then it+1's quarter 0
+      // loaded into the same registers; the B-sub 0 reads retired (B0 is restaged in p2)
+      if (ex) {
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" : "+v"(wn0));
+        bits_expand(wn0, fa0);
+      }
+      if (h1 && !ka1) load_bits<0>(pp, t, kt1);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    } else if constexpr (BITS == 1) {
       // both quarters' words (the buffer is next restaged in tile it+1's p1); the whole block of
       // it+1 into the other buffer, whose last reads were tile it-1's p1; quarter 0 expanded once
       // every read retired (B-sub 0's as well: B0 is restaged in p2)
@@ -357,7 +414,18 @@ struct E8 {
     mfma_q<0, 1>(fa0, fb1);
     sbar<3>();
     // p3 (1,1)
-    if constexpr (BITS) {
+    if constexpr (BITS == 2) {
+      // quarter 1 (loaded in the last p3: what is younger may stay in flight except this tile's
+      // B0 halves), then it+1's
+      if (ex) {
+        if (ib2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("" : "+v"(wn1));
+        bits_expand(wn1, fa1);
+      }
+      if (h1 && !ka1) load_bits<1>(pp, t, kt1);
+    } else if constexpr (BITS == 1) {
       if (ex) bits_expand(wb1, fa1);
     } else {
       if (rdf) rd_a<1, Bf>(fa1);
@@ -386,7 +454,7 @@ struct E8 {
 
 // One workgroup's tile: the k-loop and the epilogue. BITS: A from the BitMat pp.abits (its AT
 // is then immaterial: the bits path has one A layout)
-template <bool AT, bool BT, int EPI, bool TE, bool ST, bool BITS>
+template <bool AT, bool BT, int EPI, bool TE, bool ST, int BITS>
 __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
   const Params& p = pp.g;
   unsigned long long st_k0 = 0, st_k2 = 0;  // stamped builds: kernel start, k-loop end (realtime)
@@ -394,7 +462,7 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
-  const Tile t = tile_of_t<256, 256>(p, true);
+  const Tile t = tile_of_t<256, 256>(p, true, pp.dj.nworkers);
 
   using S = E8<AT, BT, ST, BITS>;
   S s;
@@ -418,8 +486,11 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) s.acc[b][i][j][k] = f32x4{0.f, 0.f, 0.f, 0.f};
   const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
-  if constexpr (BITS) {
+  if constexpr (BITS == 1) {
     s.bA = lds0 + (unsigned)(wm * 512 + lane * 8);  // quarter (0, wm): rows 64 wm .. of half 0
+  } else if constexpr (BITS == 2) {
+    s.wq = wm * 64 + lane;  // (quarter (0, wm): words 128 wm + 2 lane, + 1; quarter 1: + 256)
+    s.ready = 0;
   } else if constexpr (S::KA) {
     s.aA[0] = lds0 + frag_addr<true>(64 * wm, lane);
   } else {
@@ -434,7 +505,7 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
   }
 
   // (bits: A is exact, its residual planes zero -- the pairs with A plane 0)
-  const int np = BITS ? pp.npairs_a0 : (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
+  const int np = BITS != 0 ? pp.npairs_a0 : (pp.dyn && *pp.dyn == 0) ? pp.npairs0 : pp.npairs;
   const int nkt = t.ks < t.ke ? (t.ke - t.ks + EBK - 1) / EBK : 0;
   const int total = np * nkt;
   // waves 4-7 (the second wave of every SIMD), as a scalar condition: s_barrier ignores EXEC
@@ -449,7 +520,7 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
     // images). Cursor = (group g of two k-tiles, index r within it).
     struct Cur { int g, r, kt, pr; };
     // (the bits path walks pairs innermost: the pairs of a k-tile reuse its expanded fragments)
-    const bool rw = pp.reuse != 0 && !BITS;
+    const bool rw = pp.reuse != 0 && BITS == 0;
     auto set = [&](Cur& c) {
       if (!rw) { c.kt = c.g; c.pr = c.r; return; }
       if (2 * c.g + 1 < nkt) { c.kt = 2 * c.g + (c.r & 1); c.pr = c.r >> 1; }
@@ -474,8 +545,13 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
     // prologue: A0 B0 B1 A1 of k-tile 0, then B0 A0 B1 of k-tile 1 (its A1: tile 0's p1); the bits
     // path: k-tile 0's block, B0 B1, then k-tile 1's B0 B1 (its block: tile 0's p1)
     int kt1 = c1.kt, pr1 = c1.pr, kt2 = c2.kt, pr2 = c2.pr;
-    if constexpr (BITS) {
-      s.template issue_bits<0>(t, 0);
+    if constexpr (BITS != 0) {
+      if constexpr (BITS == 2) {
+        s.template load_bits<0>(pp, t, 0);
+        s.template load_bits<1>(pp, t, 0);
+      } else {
+        s.template issue_bits<0>(t, 0);
+      }
       s.template issue_b<0, 0>(pp, t, 0, 0);
       s.template issue_b<1, 0>(pp, t, 0, 0);
       if (total > 1) {
@@ -511,8 +587,8 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
     auto step = [&]() { cm = c0; c0 = c1; c1 = c2; adv(c2); };
     // the bits path: it+1's block is copied only for a new k-tile, and an iteration expands only
     // when its k-tile is not it-1's
-    auto ka1_of = [&](int j) { return BITS ? c1.kt == c0.kt : ka(c1, cm, j); };
-    auto ex_of = [&](int j) { return !BITS || j == 0 || c0.kt != cm.kt; };
+    auto ka1_of = [&](int j) { return BITS != 0 ? c1.kt == c0.kt : ka(c1, cm, j); };
+    auto ex_of = [&](int j) { return BITS == 0 || j == 0 || c0.kt != cm.kt; };
     for (int it = 0; it < total; it += 2) {
       s.template tile<0>(pp, t, it, total, c1.kt, c1.pr, c2.kt, c2.pr, ka1_of(it + 1), ka(c2, c0, it + 2),
                          kb(c2, c0, it + 2), ex_of(it));
@@ -578,23 +654,169 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
 template <bool BT, int EPI, bool ST>
 constexpr bool has_bits = !BT && !ST && (EPI == EPI_STORE || EPI == EPI_ACT);
 
+// The fused de-interleave's workers (DeintJob). A worker workgroup takes tasks T = w, w + W, ...
+// (task T: chunk order[T / R] of 256 pixels, batch rows 64 (T % R) ..), each in 4 passes of 16
+// rows. Waves 0-3 are loaders: each pass's 16 rows x 3 KB of X (the row chunk's interleaved
+// pixels) go HBM -> LDS by 48 LDS-DMA instructions of 1 KB each -- whole contiguous KBs (a
+// thread's own 96-B pieces at a 96-B lane stride, the standalone kernel's loads, touch 6x the
+// L1 lines they use and held a CU to ~25 GB/s) -- into a ring of 3 pass buffers, two passes in
+// flight. Waves 4-7 are consumers: per pass each thread reads two rows' octets (96 B) from LDS,
+// writes their block bytes (deint_octet) into the task's byte image, and, one task later, the
+// task's words (deint_words; forward words written through). One workgroup barrier per pass
+// orders the ring; a task is counted in done[chunk] two passes after its stores were issued,
+// behind the consumers' vmcnt(0) and that pass's barrier.
+constexpr int DW_ROWB = 64 * DEINT_FUSE_PB * 12;   // bytes of one row's 256-pixel chunk (3 KB)
+constexpr int DW_PASSB = 16 * DW_ROWB;              // one pass: 16 rows (48 KB)
+constexpr int DW_BT = 3 * 8 * DEINT_FUSE_PB * 72;   // one task's byte image (DeintLds)
+constexpr int DW_ORDER = 3 * DW_PASSB + 2 * DW_BT;  // LDS byte offset of the order table
+constexpr int DW_LDS = 163840;                      // the workgroup's LDS (160 KB)
+constexpr int DW_MAXCH = (DW_LDS - DW_ORDER) / 4;   // chunks the order table can hold
+static_assert(DW_ORDER + 4 * 64 <= DW_LDS, "LDS");
+__device__ __forceinline__ void deint_worker(const DeintJob& dj, short* smem) {
+  constexpr int PB = DEINT_FUSE_PB, OS = 72;
+  using Lds = DeintLds<PB, OS>;
+  char* lds = reinterpret_cast<char*>(smem);
+  int* ord = reinterpret_cast<int*>(lds + DW_ORDER);
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const bool loader = __builtin_amdgcn_readfirstlane(wave) < 4;
+  const int R = dj.B >> 6;
+  const int W = dj.nworkers;
+  const int ntask = dj.nchunks * R;
+  const int D = dj.D;
+  if (blockIdx.x == 0 && tid == 0 && dj.dyn_next) {
+    dj.dyn_next[0] = 0;
+    dj.dyn_next[2] = 0;
+  }
+  for (int i = tid; i < dj.nchunks; i += ENT) ord[i] = dj.order[i];
+  __syncthreads();
+  if ((int)blockIdx.x >= ntask) return;
+  const int ntw = (ntask - 1 - (int)blockIdx.x) / W + 1;  // this worker's tasks
+  const int P = 4 * ntw;                                   // ... and passes
+  auto task_of = [&](int k) { return (int)blockIdx.x + k * W; };
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  // loaders: pass p's 48 KB into ring buffer p % 3 (instruction j = row j / 3, KB j % 3 of it)
+  auto issue = [&](int p) {
+    const int T = task_of(p >> 2);
+    const int c = ord[T / R];
+    const size_t row0 = (size_t)(64 * (T % R) + 16 * (p & 3));
+    const int f0 = 3 * 256 * c;  // first float of the row chunk
+#pragma unroll
+    for (int m = 0; m < 12; ++m) {
+      const int jj = wave + 4 * m, rr = jj / 3, part = jj % 3;
+      int f = f0 + part * 256 + 4 * lane;
+      f = f + 4 <= 3 * D ? f : 3 * D - 4;  // (past the row: its last 16 B, unused)
+      const float* src = dj.x + (row0 + rr) * 3 * (size_t)D + f;
+      __builtin_amdgcn_global_load_lds(src, (lds_ptr)(lds + (p % 3) * DW_PASSB + jj * 1024), 16, 0, 0);
+    }
+  };
+  if (loader && !(dj.diag & 16)) {
+    issue(0);
+    if (P > 1) issue(1);
+  }
+  const int ct = tid - 256;  // consumer thread
+  bool nb = false;
+  int pend = -1;  // chunk of the task whose stores await their count
+  for (int p = 0; p < P; ++p) {
+    const int k = p >> 2, q = p & 3;
+    if (loader) {
+      if (p + 1 < P) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (q == 2 && pend >= 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last task's stores complete
+    }
+    // (a bare barrier: __syncthreads' release fence would wait for the loaders' DMA in flight)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    bar();
+    if (loader) {
+      if (p + 2 < P && !(dj.diag & 16)) issue(p + 2);  // into the buffer pass p - 1 was read from
+      continue;
+    }
+    if (dj.diag & 8) continue;  // (diagnostics: the loaders alone)
+    if (q == 2 && pend >= 0) {
+      if (ct == 0) __hip_atomic_fetch_add(dj.done + pend, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      pend = -1;
+    }
+    const int T = task_of(k);
+    const int c = ord[T / R], by = T % R;
+    if (q == 0 && k > 0) {  // the last task's words from its byte image
+      const int Tp = task_of(k - 1);
+      const int cp = ord[Tp / R];
+      deint_words<PB, OS, true>(ct, 256, dj.B, D, dj.kts_f, dj.kts_w, dj.xbf, dj.xbw, cp, Tp % R,
+                                *reinterpret_cast<const Lds*>(lds + 3 * DW_PASSB + ((k - 1) & 1) * DW_BT));
+      pend = cp;
+    }
+    Lds& bt = *reinterpret_cast<Lds*>(lds + 3 * DW_PASSB + (k & 1) * DW_BT);
+    const char* raw = lds + (p % 3) * DW_PASSB;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int it = ct + 256 * h, rr = it >> 5, o = it & 31;
+      const int pix = 256 * c + 8 * o, r = 16 * q + rr;
+      unsigned by3[3];
+      const unsigned pad = (pix <= D && D < pix + 8) ? 1u << (D - pix) : 0u;
+      by3[0] = by3[1] = by3[2] = pad;
+      if (pix + 8 <= D) {
+        const float4* src = reinterpret_cast<const float4*>(raw + rr * DW_ROWB + o * 96);
+        float e[24];
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+          const float4 v = src[t];
+          e[4 * t] = v.x; e[4 * t + 1] = v.y; e[4 * t + 2] = v.z; e[4 * t + 3] = v.w;
+        }
+        nb |= deint_octet(e, by3);
+        dj.xbits[(size_t)(64 * by + r) * dj.ldbits + (pix >> 3)] = (unsigned char)by3[1];
+      }
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) bt[cc][o][r] = (unsigned char)by3[cc];
+    }
+  }
+  // the last task: its words once every consumer's bytes are in (the barrier), then its count
+  __syncthreads();
+  if (!loader) {
+    const int Tl = task_of(ntw - 1);
+    const int cl = ord[Tl / R];
+    deint_words<PB, OS, true>(ct, 256, dj.B, D, dj.kts_f, dj.kts_w, dj.xbf, dj.xbw, cl, Tl % R,
+                              *reinterpret_cast<const Lds*>(lds + 3 * DW_PASSB + ((ntw - 1) & 1) * DW_BT));
+    if (dj.dyn && __ballot(nb) != 0 && lane == 0) atomicOr(dj.dyn + 2, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  if (ct == 0) {
+    if (pend >= 0) __hip_atomic_fetch_add(dj.done + pend, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(dj.done + ord[task_of(ntw - 1) / R], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <bool AT, bool BT, int EPI, bool TE, bool ST = false>
 __global__ __launch_bounds__(ENT, 1) void gemm_bf16e_kernel(PParams pp) {
   if (epi_skip<EPI>(pp.g.epi)) return;
+  if (pp.g.epi.only_if && *pp.g.epi.only_if == 0) return;
   // [A0 b0 | A0 b1 | A1 b0 | A1 b1 | B0 b0 | B0 b1 | B1 b0 | B1 b1]; the row-major epilogue's two
   // 64-row bands and the BCE row partials reuse it after the k-loop (one __shared__ array: a
   // second one can make hipcc wait vmcnt(0) before the loop's LDS reads)
   constexpr int RING = 8 * EH;
   constexpr int EPIL = 2 * (2 * 64 * 256 + 64 * 4 * 32);
-  __shared__ __attribute__((aligned(1024))) short smem[RING > EPIL ? RING : EPIL];
+  // (the bits-path instantiations also carry the fused de-interleave's workers: the whole 160 KB)
+  constexpr int SM0 = RING > EPIL ? RING : EPIL;
+  constexpr int SM = has_bits<BT, EPI, ST> && DW_LDS / 2 > SM0 ? DW_LDS / 2 : SM0;
+  __shared__ __attribute__((aligned(1024))) short smem[SM];
   // a 0/1 batch (the de-interleave's not-binary word, a uniform branch): A from its bits
   if constexpr (has_bits<BT, EPI, ST>) {
+    if (pp.dj.nworkers) {  // the fused de-interleave: workers first, then the GEMM's tiles
+      if ((int)blockIdx.x < pp.dj.nworkers) {
+        if (!(pp.dj.diag & 4)) deint_worker(pp.dj, smem);
+        return;
+      }
+      if (pp.dj.diag & 2) return;
+      e8_tile<false, BT, EPI, TE, ST, 2>(pp, smem);
+      return;
+    }
     if (pp.abits && (!pp.anb || *pp.anb == 0)) {
-      e8_tile<false, BT, EPI, TE, ST, true>(pp, smem);
+      if (pp.bits_reg) e8_tile<false, BT, EPI, TE, ST, 2>(pp, smem);
+      else e8_tile<false, BT, EPI, TE, ST, 1>(pp, smem);
       return;
     }
   }
-  e8_tile<AT, BT, EPI, TE, ST, false>(pp, smem);
+  e8_tile<AT, BT, EPI, TE, ST, 0>(pp, smem);
 }
 
 template <bool AT, bool BT, int EPI, bool TE>
@@ -606,7 +828,8 @@ hipError_t launch_e(const PParams& p, hipStream_t st) {
       return hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((gemm_bf16e_kernel<AT, BT, EPI, TE>), dim3(nwg), dim3(ENT), 0, st, p);
+  if (p.dj.nworkers && (!has_bits<BT, EPI, false> || AT || !p.abits || (p.dj.nworkers & 7))) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm_bf16e_kernel<AT, BT, EPI, TE>), dim3(nwg + p.dj.nworkers), dim3(ENT), 0, st, p);
   return hipGetLastError();
 }
 

@@ -51,6 +51,8 @@ struct PParams {
   long long abits_sb = 0;
   const int* anb = nullptr;
   int npairs_a0 = 1;                // the leading pairs with A plane 0 (the bits path's pairs)
+  DeintJob dj;                      // eight-phase kernel: the fused de-interleave (GemmDesc::dj)
+  int bits_reg = 0;                 // eight-phase bits path: A words by loads to registers (E8 BITS 2)
 };
 
 // tanh as an odd [13/6] rational in x on [-7.905, 7.905] (clamped beyond, where tanh rounds to
@@ -169,11 +171,14 @@ struct Tile {
   int z, bi, si, m0, n0, nt, ks, ke;
 };
 template <int TBM, int TBN>
-__device__ __forceinline__ Tile tile_of_t(const Params& p, bool remap) {
+__device__ __forceinline__ Tile tile_of_t(const Params& p, bool remap, int boff = 0) {
   Tile t;
   const int tiles = p.ntm * p.ntn;
   const int nwg = tiles * p.batch * p.split;
-  const int b = remap ? xcd_remap(blockIdx.x, nwg) : (int)blockIdx.x;
+  // boff: workgroups ahead of the tiles (the fused de-interleave's workers; a multiple of 8, so
+  // blockIdx % 8 still names the XCD)
+  const int bx = (int)blockIdx.x - boff;
+  const int b = remap ? xcd_remap(bx, nwg) : bx;
   t.z = b / tiles;
   const int rem = b - t.z * tiles;
   int mt;

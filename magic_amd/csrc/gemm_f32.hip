@@ -202,6 +202,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(Params p) {
 template <int EPI>
 __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, int M, int N,
                                      float* __restrict__ C, int ldc, long long sC, GemmEpi e) {
+  if (e.only_if && *e.only_if == 0) return;
   const int bi = blockIdx.z;
   const long long slab = (long long)M * N;
   const float* w = ws + (size_t)bi * split * slab;
@@ -241,6 +242,7 @@ __global__ void splitk_reduce_kernel(const float* __restrict__ ws, int split, in
 template <int EPI>
 __global__ void splitk_reduce4_kernel(const float* __restrict__ ws, int split, int M, int N,
                                       float* __restrict__ C, int ldc, long long sC, GemmEpi e) {
+  if (e.only_if && *e.only_if == 0) return;
   const int bi = blockIdx.z;
   const long long slab = (long long)M * N;
   const float* w = ws + (size_t)bi * split * slab;

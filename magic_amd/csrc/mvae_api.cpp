@@ -133,6 +133,13 @@ struct mvae_ctx {
   unsigned* xbf = nullptr;
   unsigned* xbw = nullptr;
   int kts_f = 0, kts_w = 0;
+  // the de-interleave inside the layer-0 forward's launch (create option deint_fuse; DeintJob):
+  // f0f the fused launch (bits path, its own split), f0fb the plane-path fallback that runs only
+  // for a batch with a pixel other than 0 / 1; fuse_buf: the chunk counters, error word, order
+  bool fuse = false;
+  GemmDesc f0f, f0fb;
+  int* fuse_buf = nullptr;
+  int fuse_nchunks = 0;
   // schedule (each GEMM tagged with its timing region)
   std::vector<GemmDesc> fwd_enc;  // encoder layers + head
   // the hidden layers fwd_enc[1 .. nenc-1] as one launch (enc_chain.hip; create option enc_chain)
@@ -450,6 +457,9 @@ struct CreateOpts {
   int diag_chain = 0;      // ... its timing ablations (ChainArgs::diag; results meaningless)
   int dec_chain = 1;    // bf16 mode: the decoder's two hidden layers in one launch (0: one GEMM each)
   int bits = 1;         // plane modes: the layer-0 pixel operand of a 0/1 batch as bits (BitMat)
+  int bits_reg = 0;     // ... the eight-phase bits path loading A's words to registers (E8 BITS 2)
+  int deint_fuse = 0;   // ... the de-interleave run inside the layer-0 forward's launch (DeintJob)
+  int deint_fuse_diag = 0;  // ... its timing diagnostics (DeintJob::diag; results invalid)
   int conv2_nw = 8, conv2_tpb = 1, conv2_fpw = 2, conv2_wg = 8, conv2_half = 1, conv2_nchunk = 0;
 };
 
@@ -483,6 +493,9 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "diag_chain" && in(0, 7)) o->diag_chain = (int)v;
     else if (k == "dec_chain" && in(0, 1)) o->dec_chain = (int)v;
     else if (k == "bits" && in(0, 1)) o->bits = (int)v;
+    else if (k == "bits_reg" && in(0, 1)) o->bits_reg = (int)v;
+    else if (k == "deint_fuse" && in(0, 1)) o->deint_fuse = (int)v;
+    else if (k == "deint_fuse_diag" && in(0, 31)) o->deint_fuse_diag = (int)v;
     else if (k == "enc_chain_rows" && (v == 0 || (in(16, 96) && v % 16 == 0))) o->enc_chain_rows = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
     else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
@@ -840,6 +853,7 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
       // the weight gradient's batch 2 (g2) reads stacked rows B .. 3B: k-tiles from B / 64
       w0.Abits = c->xbw; w0.abits_kts = c->kts_w; w0.anb = c->dyn + 2;
       w0.abits_sb = (long long)(c->B / 64) * BITMAT_BLOCK_WORDS;
+      f0.bits_reg = w0.bits_reg = opt.bits_reg;
       c->bits_on = true;
     }
   }
@@ -907,8 +921,63 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
       c->f_split = true;
     }
   }
+  {  // the de-interleave inside the layer-0 forward's launch (DeintJob): the forward's 256 x 256
+     // tiles x split leave CUs free for its workers (C3: 192 tiles + 64 workers; C2: 96 tiles x
+     // split 2 + 64 workers), so its HBM stream runs beside the k-loop instead of before it
+    const GemmDesc& f0 = c->fwd_enc[0];
+    const long long tiles = (long long)((f0.M + 255) / 256) * ((f0.N + 255) / 256) * f0.batch;
+    const int kt = (f0.K + 63) / 64;
+    int sp = 0;  // the largest split whose workgroups leave >= 32 CUs (>= 8 k-tiles per slab)
+    for (int s = 1; s <= 8 && tiles * s <= 224 && (s == 1 || kt / s >= 8); ++s) sp = s;
+    int sp_plan = 0, tn = 0, tm = 0;
+    if (c->bits_on) gemm_bf16_wide_plan(f0, ~size_t(0), &sp_plan, &tn, &tm);
+    if (opt.deint_fuse && c->bits_on && sp > 0 && f0.batch == 1 && tn == GEMM_TN_E8 && !f0.at && !f0.bt &&
+        (f0.epi.mode == EPI_ACT || f0.epi.mode == EPI_STORE) && (c->D % 8) == 0 && (c->ldx % 8) == 0) {
+      const int nwg = (int)tiles * sp;
+      const int W = (256 - nwg) & ~7;
+      const int nch = (c->kts_f + DEINT_FUSE_PB - 1) / DEINT_FUSE_PB;
+      if (nch > 640) goto no_fuse;  // (the workers' LDS order table: gemm_bf16e.hip DW_MAXCH)
+      float* q = nullptr;
+      ALLOC(q, 2 * (size_t)nch + 8);
+      c->fuse_buf = reinterpret_cast<int*>(q);
+      // production order: by the slab-local k-tile at which a consumer first needs the chunk (the
+      // split-K slabs' chunks in turn), then by chunk
+      const int kcs = (kt + sp - 1) / sp;  // k-tiles per slab
+      std::vector<std::pair<int, int>> key(nch);
+      for (int ch = 0; ch < nch; ++ch) {
+        const int k0 = DEINT_FUSE_PB * ch, sl = std::min(sp - 1, k0 / kcs);
+        key[ch] = {k0 - sl * kcs, ch};
+      }
+      std::sort(key.begin(), key.end());
+      std::vector<int> order(nch);
+      for (int i = 0; i < nch; ++i) order[i] = key[i].second;
+      if (hipMemcpy(c->fuse_buf + nch + 8, order.data(), nch * sizeof(int), hipMemcpyHostToDevice) != hipSuccess) {
+        g_create_err = "hipMemcpy fuse order";
+        mvae_destroy(c);
+        return MVAE_EINVAL;
+      }
+      GemmDesc f = f0;
+      f.split = sp;
+      f.variant = 13;  // the eight-phase kernel (its bits path carries the workers)
+      DeintJob& j = f.dj;
+      j.B = c->B; j.D = c->D; j.kts_f = c->kts_f; j.kts_w = c->kts_w;
+      j.xbf = c->xbf; j.xbw = c->xbw; j.xbits = c->xbits; j.ldbits = c->ldbits;
+      j.done = c->fuse_buf;
+      j.err = c->fuse_buf + nch;
+      j.order = c->fuse_buf + nch + 8;
+      j.nworkers = W;
+      j.nchunks = nch;
+      j.diag = opt.deint_fuse_diag;
+      c->f0f = f;
+      c->f0fb = f0;  // (epi.only_if: the not-binary word, set per call)
+      c->fuse_nchunks = nch;
+      c->fuse = true;
+    }
+  no_fuse:;
+  }
   size_t ws = 0;
   auto wsz = [&](const GemmDesc& d) { ws = std::max(ws, gemm_workspace_elems(d)); };
+  if (c->fuse) wsz(c->f0f);
   for (int R : {2, 4, 8})
     for (auto& d : c->w0c[R]) wsz(d);
   for (auto& d : c->fwd_enc) wsz(d);
@@ -1216,7 +1285,35 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
     MV_CHECK(hipEventRecord(c->sync_ev[c->sync_next % c->sync_ev.size()], c->stage));
     MV_CHECK(hipStreamWaitEvent(st, c->sync_ev[c->sync_next++ % c->sync_ev.size()], 0));
   }
-  if (!(c->diag_skip_deint && c->dyn_cur)) {  // (diagnostics: the stale image of the last pass)
+  bool f0_done = false;  // the layer-0 forward ran with the fused de-interleave
+  if (c->fuse && !c->diag_skip_deint && !c->diag_shadow && (reinterpret_cast<uintptr_t>(x) % 16) == 0) {
+    // one launch: the de-interleave's workers beside the forward GEMM's tiles (DeintJob); then the
+    // grey pass (zeroing the chunk counters) and the forward on the planes, both returning at once
+    // for a 0/1 batch
+    int* prev = c->dyn_cur ? c->dyn_cur : c->dyn;
+    int* cur = prev == c->dyn ? c->dyn + 1 : c->dyn;
+    {
+      TIMED("deint_fwd0");
+      GemmDesc f = c->f0f;
+      f.dj.x = x;
+      f.dj.dyn = cur;
+      f.dj.dyn_next = prev;
+      if (f.dynA == c->dyn) f.dynA = cur;
+      MV_CHECK(gemm_run(f, c->ws, c->ws_elems, st));
+    }
+    {
+      TIMED("deint_grey");
+      MV_CHECK(launch_deint_grey(x, c->B, c->D, cur, c->xs, planes_of(c, c->xs), c->ldx, c->x32dyn, c->fuse_buf,
+                                 c->fuse_nchunks, st));
+      GemmDesc fb = c->f0fb;
+      if (fb.dynA == c->dyn) fb.dynA = cur;
+      fb.anb = cur + 2;
+      fb.epi.only_if = cur + 2;
+      MV_CHECK(gemm_run(fb, c->ws, c->ws_elems, st));
+    }
+    c->dyn_cur = cur;
+    f0_done = true;
+  } else if (!(c->diag_skip_deint && c->dyn_cur)) {  // (diagnostics: the stale image of the last pass)
     TIMED("deinterleave");
     // the flag's slots alternate: this pass raises the one the previous pass zeroed and zeroes
     // the previous one (its readers are all behind on this stream), no memset launch per step
@@ -1271,7 +1368,7 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
       MV_CHECK(launch_lrn2_pool2_fwd(T, nimg, c->xf, c->ldf, c->xf32, planes_of(c, c->xf), st));
     }
   }
-  for (size_t i = 0; i < c->fwd_enc.size(); ++i) {
+  for (size_t i = f0_done ? 1 : 0; i < c->fwd_enc.size(); ++i) {
     if (c->chain && i == 1) {  // the hidden layers 1 .. nenc-1
       TimeScope ts(c, c->chain_r, st);
       MV_CHECK(launch_enc_chain(c->chain_args, st));
@@ -1788,6 +1885,7 @@ extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int
     if (e == hipSuccess) e = hipMemsetAsync(pnb, 0, 16, st);
     if (e == hipSuccess) e = launch_bits_from_plane(d.Ap, lda, at != 0, M, K, (unsigned*)pbits, kts, (int*)pnb, st);
     d.Abits = (const unsigned*)pbits; d.abits_kts = kts; d.anb = (const int*)pnb;
+    d.bits_reg = (epi >> 15) & 1;  // epi bit 15: its words loaded to registers (E8 BITS 2)
   }
   // epi bit 12 (plane modes): the output as bf16 planes only (no fp32 store), as the step's
   // producers write their operand images; C then receives the planes' sum (host side)

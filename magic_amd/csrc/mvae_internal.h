@@ -68,7 +68,38 @@ struct GemmEpi {
   // its constant value: 1.0 at column N when padw == 2 (an activation's ones column), else 0.
   // (Element-wise stores of a partial last chunk cost ~5 us per 256x256-tile epilogue.)
   int padw = 0;
+  // the launch (and a split-K reduction's) returns at entry while *only_if == 0: the layer-0
+  // forward's plane-path fallback behind the fused de-interleave (DeintJob), which runs only for a
+  // batch with a pixel other than 0 or 1 (eight-phase kernel and split-K reductions only)
+  const int* only_if = nullptr;
 };
+
+// The de-interleave to bits run inside the layer-0 forward's launch (create option deint_fuse):
+// workgroups [0, nworkers) are workers that de-interleave tasks of 64 batch rows x 256 pixels
+// (deint_bits.h) chunk by chunk, in `order`, writing the forward BitMat through (`sc1`) and
+// counting each finished task in done[chunk] by an agent-scope atomic add after every storing
+// wave's vmcnt(0); the GEMM workgroups (the rest, tile = block - nworkers) read the BitMat's words
+// by `sc1` loads to registers, each wave after its own `sc1` poll of done[chunk] reached B / 64
+// (MI355X_MICROARCH.md's sc1 hand-off, first row). The forward GEMM's tiles x split leave
+// nworkers CUs free, so the de-interleave's HBM stream runs beside the k-loop instead of before
+// it. A wait longer than ~0.5 s raises *err and proceeds (results then invalid; never a hang).
+struct DeintJob {
+  const float* x = nullptr;
+  int B = 0, D = 0, kts_f = 0, kts_w = 0;
+  unsigned* xbf = nullptr;
+  unsigned* xbw = nullptr;
+  unsigned char* xbits = nullptr;
+  int ldbits = 0;
+  int* dyn = nullptr;
+  int* dyn_next = nullptr;
+  int* done = nullptr;         // [nchunks], zero at launch (deint_grey_kernel zeroes it after)
+  const int* order = nullptr;  // [nchunks] chunk production order (the split-K slabs' chunks in turn)
+  int* err = nullptr;
+  int nworkers = 0, nchunks = 0;  // nworkers 0: no fused de-interleave
+  int diag = 0;  // timing diagnostics (results invalid): 1 tiles do not wait, 2 tiles exit at once,
+                 // 4 workers exit at once, 8 workers' consumers idle, 16 workers' loaders idle
+};
+constexpr int DEINT_FUSE_PB = 4;  // k-tiles (64 pixels each) per chunk
 
 // bf16 operand shadows (precision = bf16). When set, the GEMM reads A/B from these
 // instead of the fp32 pointers (same logical layout/ld) and accumulates in fp32.
@@ -100,6 +131,8 @@ struct GemmDesc {
   int abits_kts = 0;
   long long abits_sb = 0;
   const int* anb = nullptr;
+  DeintJob dj;                         // the fused de-interleave (eight-phase bits path only)
+  int bits_reg = 0;                    // bits path: A words by loads to registers (gemm_bf16e.hip E8)
   GemmEpi epi;
 };
 
@@ -190,6 +223,9 @@ hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int*
 // (a gated second kernel) the planes of xp, the fp32 rows of f32dyn_mask and the inexact flag as
 // launch_deinterleave writes them. dyn_next: the other flag slot, zeroed. Both BitMats must be
 // zero-filled once (their padding is never written).
+// the grey pass alone (after a fused launch: also zeroes its chunk counters done[0 .. ndone))
+hipError_t launch_deint_grey(const float* x, int B, int D, int* dyn, float* xs, const Planes& xp, int ldx,
+                             int f32dyn_mask, int* done, int ndone, hipStream_t st);
 hipError_t launch_deint_bits(const float* x, int B, int D, unsigned* xbf, int kts_f, unsigned* xbw, int kts_w,
                              unsigned char* xbits, int ldbits, int* dyn, int* dyn_next, float* xs,
                              const Planes& xp, int ldx, int f32dyn_mask, hipStream_t st, int variant = 0);

@@ -7,6 +7,7 @@
 // cost gradient (rotated+lock) and the metric gradient (lock+key) each use a CONTIGUOUS
 // 2B-row range. The backward stacks 4B rows: [rot(g1) | lock(g1) | lock(g2) | key(g2)].
 #include "mvae_internal.h"
+#include "deint_bits.h"
 #include <cstdlib>
 
 namespace mvae {
@@ -831,127 +832,32 @@ __global__ __launch_bounds__(256) void make_batch4_kernel(const unsigned char* _
 }
 
 // ---------------------------------------------------------------- de-interleave to bits
-// The layer-0 pixel operand of a 0/1 batch as the eight-phase kernel's BitMats (mvae_internal.h):
-// xbf = A of the forward (rows [rot | lock | key] x pixels, the ones column at k = D), xbw = A of
-// the weight gradient (pixels x rows, the ones row at pixel D), plus the BCE target (the lock
-// block) as bits per row (GemmEpi::xbits) -- 1.1 bits written per pixel triple instead of the 48
-// of the bf16 plane. One workgroup: 64 batch rows x 128 pixels (two k-tiles / two 64-pixel
-// quarters). Each thread reads 4 x 96 contiguous bytes (8 pixels of one row, as the plane kernel),
-// writes one byte per block into LDS ([block][octet][row]: a row-contiguous 8 x 8 bit block is one
-// u64), then assembles 3 forward and 3 weight-gradient words, stored 512 B contiguous per block.
-// Raises the not-binary word (*dyn slot 2) when a pixel is neither 0 nor 1: the step then runs
-// deint_grey_kernel (the planes) and the GEMMs read the planes. Padding outside the written
-// blocks (rows past 3B, pixel quarters past D) is zero from the buffers' creation.
-// bits el = 0..7 of b -> positions 0..3 (even el) and 16..19 (odd el): a BitMat word's layout
-__device__ __forceinline__ unsigned bits_spread(unsigned b) {
-  unsigned e = b & 0x55u, o = (b >> 1) & 0x55u;
-  e = (e | (e >> 1)) & 0x33u; e = (e | (e >> 2)) & 0x0Fu;
-  o = (o | (o >> 1)) & 0x33u; o = (o | (o >> 2)) & 0x0Fu;
-  return e | (o << 16);
-}
-// PB k-tiles (64 PB pixels) per workgroup of NT threads; OS: LDS bytes per octet row (72: the 16
-// octets of a write land on 16 banks)
+// The layer-0 pixel operand of a 0/1 batch as BitMats (deint_bits.h): one workgroup per task of
+// 64 batch rows x 64 PB pixels. Raises the not-binary word (*dyn slot 2) when a pixel is neither 0
+// nor 1: the step then runs deint_grey_kernel (the planes) and the GEMMs read the planes.
 template <int PB, int NT, int OS>
 __global__ __launch_bounds__(NT) void deint_bits_kernel(const float4* __restrict__ x, int B, int D, int kts_f,
                                                         int kts_w, unsigned* __restrict__ xbf,
                                                         unsigned* __restrict__ xbw,
                                                         unsigned char* __restrict__ xbits, int ldbits,
                                                         int* __restrict__ dyn, int* __restrict__ dyn_next) {
-  constexpr int NO = 8 * PB;          // octets per row
-  constexpr int RPP = NT / NO;        // rows per pass
-  constexpr int NR = 64 / RPP;        // row passes per thread
-  static_assert(NT % NO == 0 && 64 % RPP == 0, "whole rows per pass");
   if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) dyn_next[0] = dyn_next[2] = 0;
-  __shared__ __attribute__((aligned(16))) unsigned char bt[3][NO][OS];  // [block][octet][row]
-  const int tid = threadIdx.x;
-  const int b0 = blockIdx.y * 64, p0 = blockIdx.x * 64 * PB;
-  const int o = tid % NO, pix = p0 + 8 * o;
-  const bool in = pix + 8 <= D;
-  float4 v[NR][6];
-  if (in) {
-#pragma unroll
-    for (int i = 0; i < NR; ++i) {
-      const float4* src = x + ((size_t)(b0 + tid / NO + RPP * i) * 3 * D + 3 * (size_t)pix) / 4;
-#pragma unroll
-      for (int k = 0; k < 6; ++k) v[i][k] = src[k];
-    }
-  }
-  bool nb = false;
-  // pixels past D: the ones column (pixel D) and zeros
-  const unsigned pad = (pix <= D && D < pix + 8) ? 1u << (D - pix) : 0u;
-#pragma unroll
-  for (int i = 0; i < NR; ++i) {
-    const int r = tid / NO + RPP * i;
-    unsigned by[3] = {pad, pad, pad};
-    if (in) {
-      const float e[24] = {v[i][0].x, v[i][0].y, v[i][0].z, v[i][0].w, v[i][1].x, v[i][1].y, v[i][1].z, v[i][1].w,
-                           v[i][2].x, v[i][2].y, v[i][2].z, v[i][2].w, v[i][3].x, v[i][3].y, v[i][3].z, v[i][3].w,
-                           v[i][4].x, v[i][4].y, v[i][4].z, v[i][4].w, v[i][5].x, v[i][5].y, v[i][5].z, v[i][5].w};
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const int ch = c == 0 ? 1 : (c == 1 ? 0 : 2);  // block c (rot, lock, key) <- channel ch
-        unsigned byte = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float f = e[3 * j + ch];
-          byte |= (f != 0.f ? 1u : 0u) << j;
-          nb |= (f != 0.f) & (f != 1.f);
-        }
-        by[c] = byte;
-      }
-      xbits[(size_t)(b0 + r) * ldbits + (pix >> 3)] = (unsigned char)by[1];
-    }
-#pragma unroll
-    for (int c = 0; c < 3; ++c) bt[c][o][r] = (unsigned char)by[c];
-  }
-  if (dyn) {
-    const bool anb = __ballot(nb) != 0;
-    if ((tid & 63) == 0 && anb) atomicOr(dyn + 2, 1);
-  }
-  __syncthreads();
-  // 3 blocks x PB (k-tiles / pixel quarters) x 128 words of each BitMat
-  for (int wi = tid; wi < 3 * PB * 128; wi += NT) {
-    const int c = wi / (PB * 128), kk = (wi / 128) % PB, wl = wi & 127, lane = wl >> 1, j = wl & 1;
-    const int grow = c * B + b0;  // first stacked row of this workgroup's 64
-    // forward: rows 16 (2 j + h) + (lane & 15), k-octet 8 kk + 4 kh + (lane >> 4)
-    const int kt = PB * blockIdx.x + kk;
-    if (kt < kts_f) {
-      unsigned w = 0;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh)
-          w |= bits_spread(bt[c][8 * kk + 4 * kh + (lane >> 4)][16 * (2 * j + h) + (lane & 15)]) << (8 * h + 4 * kh);
-      xbf[((size_t)(grow >> 8) * kts_f + kt) * BITMAT_BLOCK_WORDS + ((grow >> 6) & 3) * 128 + wl] = w;
-    }
-    // weight gradient: pixel 64 kk + 16 (2 j + h) + (lane & 15) of this block's, rows
-    // 32 kh + 8 (lane >> 4) + 0..7 -- bit (pixel & 7) of 8 row bytes of one octet
-    const int pq = p0 + 64 * kk;
-    if (pq <= D) {
-      unsigned w = 0;
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int kh = 0; kh < 2; ++kh) {
-          const int pr = 64 * kk + 16 * (2 * j + h) + (lane & 15);
-          const unsigned long long rows =
-              *reinterpret_cast<const unsigned long long*>(&bt[c][pr >> 3][32 * kh + 8 * (lane >> 4)]);
-          const unsigned long long col = (rows >> (pr & 7)) & 0x0101010101010101ull;
-          const unsigned byte = (unsigned)((col * 0x0102040810204080ull) >> 56);  // bit i = row i
-          w |= bits_spread(byte) << (8 * h + 4 * kh);
-        }
-      xbw[((size_t)(pq >> 8) * kts_w + (grow >> 6)) * BITMAT_BLOCK_WORDS + ((pq >> 6) & 3) * 128 + wl] = w;
-    }
-  }
+  __shared__ __attribute__((aligned(16))) DeintLds<PB, OS> bt;
+  deint_bits_task<PB, NT, OS>(x, B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, blockIdx.x, blockIdx.y, bt);
 }
 
 // The plane image of a batch with a pixel other than 0 or 1 (after deint_bits_kernel raised the
 // not-binary word; else every workgroup returns at once): bf16 plane 0 (planes 1-2 of the exact
 // split too when np == 3), the fp32 rows of the blocks in f32mask, and the inexact flag (*dyn) --
 // what the plane path's GEMMs and the BCE epilogue read. Workgroups stride over the 8-pixel groups.
+// done (the fused launch's chunk counters, DeintJob::done): zeroed for the next launch, whose
+// workers count from 0 (this kernel runs after every fused launch, in stream order)
 __global__ void deint_grey_kernel(const float4* __restrict__ x, float* __restrict__ xs,
                                   unsigned short* __restrict__ xp, long long ps, int np, int f32mask,
-                                  int* __restrict__ dyn, int B, int D, int ldx) {
+                                  int* __restrict__ dyn, int B, int D, int ldx, int* __restrict__ done,
+                                  int ndone) {
+  if (done && blockIdx.x == 0)
+    for (int i = threadIdx.x; i < ndone; i += blockDim.x) done[i] = 0;
   if (dyn[2] == 0) return;
   const int nq = D / 8;
   const size_t n = (size_t)B * nq;
@@ -1045,9 +951,14 @@ hipError_t launch_deint_bits(const float* x, int B, int D, unsigned* xbf, int kt
       hipLaunchKernelGGL((deint_bits_kernel<2, 256, 72>), dim3((kts_f + 1) / 2, B / 64), dim3(256), 0, st, x4, B, D,
                          kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
   }
+  return launch_deint_grey(x, B, D, dyn, xs, xp, ldx, f32dyn_mask, nullptr, 0, st);
+}
+
+hipError_t launch_deint_grey(const float* x, int B, int D, int* dyn, float* xs, const Planes& xp, int ldx,
+                             int f32dyn_mask, int* done, int ndone, hipStream_t st) {
   // (256 workgroups striding: for a 0/1 batch every one returns at once, and fewer cost less)
   hipLaunchKernelGGL(deint_grey_kernel, dim3(256), dim3(256), 0, st, reinterpret_cast<const float4*>(x), xs,
-                     xp.p, xp.stride, xp.n, f32dyn_mask, dyn, B, D, ldx);
+                     xp.p, xp.stride, xp.n, f32dyn_mask, dyn, B, D, ldx, done, ndone);
   return hipGetLastError();
 }
 

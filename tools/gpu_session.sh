@@ -1,14 +1,19 @@
 #!/bin/bash
-# The current GPU session (overwritten per session; earlier sessions are in git history):
-#   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r6n: the round-6 tree -- whole GPU suite, smoke, per-config timed-loop kernel traces (markers
-# around the dominant region) and the default bench line (CPU baseline, PMC traffic, configs)
+# r6t: the fused workers' loaders and consumers timed apart (deint_fuse_diag 2 + 8: loaders
+# only; 2 + 16: consumers only) at C3; bits_reg A/B (the bits path's A words to registers)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-T="python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider"
-B="--no-cpu-baseline --pmc off --no-h2d --no-pipeline --no-configs --steps 20 --warmup 3 --mark-dominant"
-p() { echo "r6n_prof_$1|240|cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/gpurun_out/prof_r6n_$1 -o run -- python3 $PWD/bench.py --config $2 $B"; }
+B="--no-cpu-baseline --pmc off --no-h2d --no-pipeline --no-configs --steps 60 --warmup 5"
 bash tools/gpu_steps.sh \
-  "r6n_tests|700|$T -m gpu tests" \
-  "r6n_smoke|240|python -c 'import __graft_entry__ as g; g.smoke()'" \
-  "$(p c2 C2)" "$(p c3 C3)" "$(p c5 C5)" \
-  "r6n_bench|900|python bench.py > gpurun_out/r6n_bench.json"
+  "r6t_c3_d10|200|python bench.py --config C3 $B --create-opt deint_fuse=1,deint_fuse_diag=10" \
+  "r6t_c3_d18|200|python bench.py --config C3 $B --create-opt deint_fuse=1,deint_fuse_diag=18" \
+  "r6t_c3_d2|200|python bench.py --config C3 $B --create-opt deint_fuse=1,deint_fuse_diag=2" \
+  "r6t_c3_r0a|200|python bench.py --config C3 $B --create-opt bits_reg=0" \
+  "r6t_c3_r1a|200|python bench.py --config C3 $B --create-opt bits_reg=1" \
+  "r6t_c3_r0b|200|python bench.py --config C3 $B --create-opt bits_reg=0" \
+  "r6t_c3_r1b|200|python bench.py --config C3 $B --create-opt bits_reg=1" \
+  "r6t_c2_r0a|200|python bench.py --config C2 $B --create-opt bits_reg=0" \
+  "r6t_c2_r1a|200|python bench.py --config C2 $B --create-opt bits_reg=1" \
+  "r6t_c2_r0b|200|python bench.py --config C2 $B --create-opt bits_reg=0" \
+  "r6t_c2_r1b|200|python bench.py --config C2 $B --create-opt bits_reg=1" \
+  "r6t_c5_r0a|200|python bench.py --config C5 $B --create-opt bits_reg=0" \
+  "r6t_c5_r1a|200|python bench.py --config C5 $B --create-opt bits_reg=1"
