@@ -132,8 +132,11 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out);
  * (0/1: bf16 mode, the decoder's two hidden layers in one launch, default 1), bits (0/1: bf16 and
  * f32x modes, the layer-0 pixel operand of a 0/1 batch as one bit per pixel -- the de-interleave
  * writes BitMats instead of the bf16 plane and the eight-phase kernel expands the A fragments in
- * registers; a batch with another pixel value takes the planes; default 1). Diagnostics, results
- * meaningless: diag_skip_deint (1: de-interleave only the first batch -- a timing bound),
+ * registers; a batch with another pixel value takes the planes; default 1), bits_reg (0/1: each
+ * wave loads its A words straight to registers, else through an LDS copy of the block; default
+ * 1), deint_fuse (0/1: the de-interleave's workers inside the layer-0 forward's launch beside its
+ * tiles, handing chunks over by counters; measured slower, default 0). Diagnostics, results
+ * meaningless: deint_fuse_diag (0-31: parts of the fused launch switched off), diag_skip_deint (1: de-interleave only the first batch -- a timing bound),
  * diag_shadow_deint (-1 or a workgroup count > 0: a second de-interleave of each step's input
  * into a scratch image on a low-priority stream, launched at diag_shadow_at = 0 the forward,
  * 1 the backward, 2 the encoder backward -- the cost of staging), diag_chain (enc_chain's

@@ -656,15 +656,19 @@ constexpr bool has_bits = !BT && !ST && (EPI == EPI_STORE || EPI == EPI_ACT);
 
 // The fused de-interleave's workers (DeintJob). A worker workgroup takes tasks T = w, w + W, ...
 // (task T: chunk order[T / R] of 256 pixels, batch rows 64 (T % R) ..), each in 4 passes of 16
-// rows. Waves 0-3 are loaders: each pass's 16 rows x 3 KB of X (the row chunk's interleaved
-// pixels) go HBM -> LDS by 48 LDS-DMA instructions of 1 KB each -- whole contiguous KBs (a
-// thread's own 96-B pieces at a 96-B lane stride, the standalone kernel's loads, touch 6x the
-// L1 lines they use and held a CU to ~25 GB/s) -- into a ring of 3 pass buffers, two passes in
-// flight. Waves 4-7 are consumers: per pass each thread reads two rows' octets (96 B) from LDS,
-// writes their block bytes (deint_octet) into the task's byte image, and, one task later, the
-// task's words (deint_words; forward words written through). One workgroup barrier per pass
-// orders the ring; a task is counted in done[chunk] two passes after its stores were issued,
-// behind the consumers' vmcnt(0) and that pass's barrier.
+// rows. Each pass's 16 rows x 3 KB of X (the row chunk's interleaved pixels) go HBM -> LDS by 48
+// LDS-DMA instructions of 1 KB each (6 per wave) -- whole contiguous KBs: a thread's own 96-B
+// pieces at a 96-B lane stride, the standalone kernel's loads, touch 6x the L1 lines they use and
+// held a CU to ~25 GB/s -- into a ring of 3 pass buffers, two passes in flight. Per pass each
+// thread reads one row octet (96 B) from LDS and writes its block bytes (deint_octet) into the
+// task's byte image -- no global store in a pass: the next pass's DMA wait would wait for it too
+// (vmcnt retires in order). At a task's first pass the previous task's words (deint_words;
+// forward words written through) and target bytes are stored, and counted in done[chunk] one pass
+// later, once every wave's vmcnt wait has retired them and the pass barrier has passed.
+// Measured at C3 (r6t-r6y): the workers alone 0.69 ms on their 64 CUs (the DMA alone 0.34 ms;
+// dedicated loader waves beside 4 transposing waves 0.88), so the fused launch (0.78 ms) loses
+// to the separate de-interleave + forward (0.50 ms): the transpose's VALU and LDS work per byte
+// needs more CUs than the forward's tiles leave free. Option deint_fuse stays off.
 constexpr int DW_ROWB = 64 * DEINT_FUSE_PB * 12;   // bytes of one row's 256-pixel chunk (3 KB)
 constexpr int DW_PASSB = 16 * DW_ROWB;              // one pass: 16 rows (48 KB)
 constexpr int DW_BT = 3 * 8 * DEINT_FUSE_PB * 72;   // one task's byte image (DeintLds)
@@ -678,7 +682,6 @@ __device__ __forceinline__ void deint_worker(const DeintJob& dj, short* smem) {
   char* lds = reinterpret_cast<char*>(smem);
   int* ord = reinterpret_cast<int*>(lds + DW_ORDER);
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const bool loader = __builtin_amdgcn_readfirstlane(wave) < 4;
   const int R = dj.B >> 6;
   const int W = dj.nworkers;
   const int ntask = dj.nchunks * R;
@@ -687,69 +690,76 @@ __device__ __forceinline__ void deint_worker(const DeintJob& dj, short* smem) {
     dj.dyn_next[0] = 0;
     dj.dyn_next[2] = 0;
   }
-  for (int i = tid; i < dj.nchunks; i += ENT) ord[i] = dj.order[i];
+  for (int i = tid; i < dj.nchunks; i += ENT) ord[i] = dj.order ? dj.order[i] : i;
   __syncthreads();
   if ((int)blockIdx.x >= ntask) return;
   const int ntw = (ntask - 1 - (int)blockIdx.x) / W + 1;  // this worker's tasks
   const int P = 4 * ntw;                                   // ... and passes
   auto task_of = [&](int k) { return (int)blockIdx.x + k * W; };
   typedef __attribute__((address_space(3))) void* lds_ptr;
-  // loaders: pass p's 48 KB into ring buffer p % 3 (instruction j = row j / 3, KB j % 3 of it)
+  // pass p's 48 KB into ring buffer p % 3: this wave's instructions jj = wave + 8 m (row jj / 3,
+  // KB jj % 3 of it)
   auto issue = [&](int p) {
+    if (dj.diag & 16) return;
     const int T = task_of(p >> 2);
     const int c = ord[T / R];
     const size_t row0 = (size_t)(64 * (T % R) + 16 * (p & 3));
     const int f0 = 3 * 256 * c;  // first float of the row chunk
 #pragma unroll
-    for (int m = 0; m < 12; ++m) {
-      const int jj = wave + 4 * m, rr = jj / 3, part = jj % 3;
+    for (int m = 0; m < 6; ++m) {
+      const int jj = wave + 8 * m, rr = jj / 3, part = jj % 3;
       int f = f0 + part * 256 + 4 * lane;
       f = f + 4 <= 3 * D ? f : 3 * D - 4;  // (past the row: its last 16 B, unused)
       const float* src = dj.x + (row0 + rr) * 3 * (size_t)D + f;
       __builtin_amdgcn_global_load_lds(src, (lds_ptr)(lds + (p % 3) * DW_PASSB + jj * 1024), 16, 0, 0);
     }
   };
-  if (loader && !(dj.diag & 16)) {
-    issue(0);
-    if (P > 1) issue(1);
-  }
-  const int ct = tid - 256;  // consumer thread
+  issue(0);
+  if (P > 1) issue(1);
+  // the BCE target bytes of task t (block 1 of its byte image) to xbits, four per thread: no
+  // store in the pass loop, whose next DMA wait would also wait for the store (vmcnt is in order)
+  auto target_bytes = [&](int t, const Lds& bt) {
+    const int c = ord[t / R], r = tid >> 3, o0 = 4 * (tid & 7);
+    const int q0 = 32 * c + o0, nq = D >> 3;  // first octet of the row chunk, octets per row
+    unsigned char* dst = dj.xbits + (size_t)(64 * (t % R) + r) * dj.ldbits + q0;
+    if (q0 + 4 <= nq) {
+      *reinterpret_cast<unsigned*>(dst) = (unsigned)bt[1][o0][r] | (unsigned)bt[1][o0 + 1][r] << 8 |
+                                          (unsigned)bt[1][o0 + 2][r] << 16 | (unsigned)bt[1][o0 + 3][r] << 24;
+    } else {
+      for (int j = 0; j < 4 && q0 + j < nq; ++j) dst[j] = bt[1][o0 + j][r];
+    }
+  };
   bool nb = false;
-  int pend = -1;  // chunk of the task whose stores await their count
+  int pend = -1;  // chunk of the task whose words were stored in the last pass
   for (int p = 0; p < P; ++p) {
     const int k = p >> 2, q = p & 3;
-    if (loader) {
-      if (p + 1 < P) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (q == 2 && pend >= 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last task's stores complete
-    }
-    // (a bare barrier: __syncthreads' release fence would wait for the loaders' DMA in flight)
+    // pass p landed; what is younger: pass p+1's DMA, issued at the end of pass p-1 (the stores
+    // of pass p-1, issued before it, retire here too)
+    if (p + 1 < P) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (a bare barrier: __syncthreads' release fence would wait for the DMA in flight)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     bar();
-    if (loader) {
-      if (p + 2 < P && !(dj.diag & 16)) issue(p + 2);  // into the buffer pass p - 1 was read from
-      continue;
-    }
-    if (dj.diag & 8) continue;  // (diagnostics: the loaders alone)
-    if (q == 2 && pend >= 0) {
-      if (ct == 0) __hip_atomic_fetch_add(dj.done + pend, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // (the words stored at the last pass are older than pass p+1's DMA: retired by this pass's
+    // wait in every wave)
+    if (pend >= 0) {
+      if (tid == 0 && dj.done) __hip_atomic_fetch_add(dj.done + pend, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       pend = -1;
     }
     const int T = task_of(k);
     const int c = ord[T / R], by = T % R;
-    if (q == 0 && k > 0) {  // the last task's words from its byte image
+    if (q == 0 && k > 0 && !(dj.diag & 8)) {  // the last task's words from its byte image
       const int Tp = task_of(k - 1);
       const int cp = ord[Tp / R];
-      deint_words<PB, OS, true>(ct, 256, dj.B, D, dj.kts_f, dj.kts_w, dj.xbf, dj.xbw, cp, Tp % R,
-                                *reinterpret_cast<const Lds*>(lds + 3 * DW_PASSB + ((k - 1) & 1) * DW_BT));
+      const Lds& btp = *reinterpret_cast<const Lds*>(lds + 3 * DW_PASSB + ((k - 1) & 1) * DW_BT);
+      deint_words<PB, OS, true>(tid, ENT, dj.B, D, dj.kts_f, dj.kts_w, dj.xbf, dj.xbw, cp, Tp % R, btp);
+      target_bytes(Tp, btp);
       pend = cp;
     }
-    Lds& bt = *reinterpret_cast<Lds*>(lds + 3 * DW_PASSB + (k & 1) * DW_BT);
-    const char* raw = lds + (p % 3) * DW_PASSB;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int it = ct + 256 * h, rr = it >> 5, o = it & 31;
+    if (!(dj.diag & 8)) {
+      Lds& bt = *reinterpret_cast<Lds*>(lds + 3 * DW_PASSB + (k & 1) * DW_BT);
+      const char* raw = lds + (p % 3) * DW_PASSB;
+      const int rr = tid >> 5, o = tid & 31;
       const int pix = 256 * c + 8 * o, r = 16 * q + rr;
       unsigned by3[3];
       const unsigned pad = (pix <= D && D < pix + 8) ? 1u << (D - pix) : 0u;
@@ -763,27 +773,37 @@ __device__ __forceinline__ void deint_worker(const DeintJob& dj, short* smem) {
           e[4 * t] = v.x; e[4 * t + 1] = v.y; e[4 * t + 2] = v.z; e[4 * t + 3] = v.w;
         }
         nb |= deint_octet(e, by3);
-        dj.xbits[(size_t)(64 * by + r) * dj.ldbits + (pix >> 3)] = (unsigned char)by3[1];
       }
 #pragma unroll
       for (int cc = 0; cc < 3; ++cc) bt[cc][o][r] = (unsigned char)by3[cc];
     }
+    // into the buffer pass p - 1 was read from (free since the barrier), after this pass's stores
+    // (issued at the pass's start, the DMA measured slower: 0.77 vs 0.69 ms of workers at C3)
+    if (p + 2 < P) issue(p + 2);
   }
-  // the last task: its words once every consumer's bytes are in (the barrier), then its count
-  __syncthreads();
-  if (!loader) {
-    const int Tl = task_of(ntw - 1);
-    const int cl = ord[Tl / R];
-    deint_words<PB, OS, true>(ct, 256, dj.B, D, dj.kts_f, dj.kts_w, dj.xbf, dj.xbw, cl, Tl % R,
-                              *reinterpret_cast<const Lds*>(lds + 3 * DW_PASSB + ((ntw - 1) & 1) * DW_BT));
-    if (dj.dyn && __ballot(nb) != 0 && lane == 0) atomicOr(dj.dyn + 2, 1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the last task: its words once every wave's bytes are in (the barrier), then its count
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  bar();
+  const int Tl = task_of(ntw - 1);
+  const int cl = ord[Tl / R];
+  if (!(dj.diag & 8)) {
+    const Lds& btl = *reinterpret_cast<const Lds*>(lds + 3 * DW_PASSB + ((ntw - 1) & 1) * DW_BT);
+    deint_words<PB, OS, true>(tid, ENT, dj.B, D, dj.kts_f, dj.kts_w, dj.xbf, dj.xbw, cl, Tl % R, btl);
+    target_bytes(Tl, btl);
   }
+  if (dj.dyn && __ballot(nb) != 0 && lane == 0) atomicOr(dj.dyn + 2, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (ct == 0) {
+  if (tid == 0 && dj.done) {
     if (pend >= 0) __hip_atomic_fetch_add(dj.done + pend, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_fetch_add(dj.done + ord[task_of(ntw - 1) / R], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(dj.done + cl, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+}
+
+// the workers alone, one per CU (diagnostics: mvae_bench_deint variant 5; order null = identity)
+__global__ __launch_bounds__(ENT, 1) void deint_persist_kernel(DeintJob dj) {
+  __shared__ __attribute__((aligned(1024))) short smem[DW_LDS / 2];
+  deint_worker(dj, smem);
 }
 
 template <bool AT, bool BT, int EPI, bool TE, bool ST = false>
@@ -845,6 +865,16 @@ template <int EPI>
 hipError_t launch_e_t(const PParams& p, bool at, bool bt, bool te, hipStream_t st) {
   return te ? launch_e_l<EPI, true>(p, at, bt, st) : launch_e_l<EPI, false>(p, at, bt, st);
 }
+
+}  // namespace
+
+hipError_t launch_deint_persist(const DeintJob& j, hipStream_t st) {
+  if (j.nworkers <= 0 || j.nchunks > DW_MAXCH || (j.B % 64) || (j.D % 8)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(deint_persist_kernel, dim3(j.nworkers), dim3(ENT), 0, st, j);
+  return hipGetLastError();
+}
+
+namespace {
 
 // (tests / diagnostics) one BitMat word per thread from a bf16 plane of 0/1 values
 __global__ void bits_from_plane_kernel(const unsigned short* __restrict__ plane, int ld, int trans, int M,

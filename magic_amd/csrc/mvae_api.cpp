@@ -457,7 +457,8 @@ struct CreateOpts {
   int diag_chain = 0;      // ... its timing ablations (ChainArgs::diag; results meaningless)
   int dec_chain = 1;    // bf16 mode: the decoder's two hidden layers in one launch (0: one GEMM each)
   int bits = 1;         // plane modes: the layer-0 pixel operand of a 0/1 batch as bits (BitMat)
-  int bits_reg = 0;     // ... the eight-phase bits path loading A's words to registers (E8 BITS 2)
+  int bits_reg = 1;     // ... the eight-phase bits path loading A's words to registers (E8 BITS 2;
+                        // 0: through an LDS copy -- C3 1.784 vs 1.769 ms, C5 2.450 vs 2.432, r6t)
   int deint_fuse = 0;   // ... the de-interleave run inside the layer-0 forward's launch (DeintJob)
   int deint_fuse_diag = 0;  // ... its timing diagnostics (DeintJob::diag; results invalid)
   int conv2_nw = 8, conv2_tpb = 1, conv2_fpw = 2, conv2_wg = 8, conv2_half = 1, conv2_nchunk = 0;

@@ -100,6 +100,8 @@ struct DeintJob {
                  // 4 workers exit at once, 8 workers' consumers idle, 16 workers' loaders idle
 };
 constexpr int DEINT_FUSE_PB = 4;  // k-tiles (64 pixels each) per chunk
+// (diagnostics) the fused launch's workers alone, j.nworkers workgroups (j.done may be null)
+hipError_t launch_deint_persist(const DeintJob& j, hipStream_t st);
 
 // bf16 operand shadows (precision = bf16). When set, the GEMM reads A/B from these
 // instead of the fp32 pointers (same logical layout/ld) and accumulates in fp32.

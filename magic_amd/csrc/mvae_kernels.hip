@@ -931,6 +931,16 @@ hipError_t launch_deint_bits(const float* x, int B, int D, unsigned* xbf, int kt
     return hipErrorInvalidValue;
   const float4* x4 = reinterpret_cast<const float4*>(x);
   switch (variant) {  // (diagnostics: mvae_bench_deint) 0 = the step's form
+    case 5: {  // the fused launch's LDS-DMA workers alone, one per CU
+      DeintJob j;
+      j.x = x; j.B = B; j.D = D; j.kts_f = kts_f; j.kts_w = kts_w;
+      j.xbf = xbf; j.xbw = xbw; j.xbits = xbits; j.ldbits = ldbits; j.dyn = dyn; j.dyn_next = dyn_next;
+      j.nchunks = (kts_f + DEINT_FUSE_PB - 1) / DEINT_FUSE_PB;
+      j.nworkers = 256;
+      const hipError_t e = launch_deint_persist(j, st);
+      if (e != hipSuccess) return e;
+      break;
+    }
     case 1:
       hipLaunchKernelGGL((deint_bits_kernel<2, 256, 64>), dim3((kts_f + 1) / 2, B / 64), dim3(256), 0, st, x4, B, D,
                          kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
