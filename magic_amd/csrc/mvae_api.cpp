@@ -136,6 +136,7 @@ struct mvae_ctx {
   // the de-interleave inside the layer-0 forward's launch (create option deint_fuse; DeintJob):
   // f0f the fused launch (bits path, its own split), f0fb the plane-path fallback that runs only
   // for a batch with a pixel other than 0 / 1; fuse_buf: the chunk counters, error word, order
+  int adam_nt = 0;  // create option adam_nt
   bool fuse = false;
   GemmDesc f0f, f0fb;
   int* fuse_buf = nullptr;
@@ -461,6 +462,7 @@ struct CreateOpts {
                         // 0: through an LDS copy -- C3 1.784 vs 1.769 ms, C5 2.450 vs 2.432, r6t)
   int deint_fuse = 0;   // ... the de-interleave run inside the layer-0 forward's launch (DeintJob)
   int deint_fuse_diag = 0;  // ... its timing diagnostics (DeintJob::diag; results invalid)
+  int adam_nt = 1;      // Adam's moment / fp32 parameter stores non-temporal (C2 -0.6 %, C3 -0.3 %, r6za)
   int conv2_nw = 8, conv2_tpb = 1, conv2_fpw = 2, conv2_wg = 8, conv2_half = 1, conv2_nchunk = 0;
 };
 
@@ -497,6 +499,7 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "bits_reg" && in(0, 1)) o->bits_reg = (int)v;
     else if (k == "deint_fuse" && in(0, 1)) o->deint_fuse = (int)v;
     else if (k == "deint_fuse_diag" && in(0, 31)) o->deint_fuse_diag = (int)v;
+    else if (k == "adam_nt" && in(0, 1)) o->adam_nt = (int)v;
     else if (k == "enc_chain_rows" && (v == 0 || (in(16, 96) && v % 16 == 0))) o->enc_chain_rows = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
     else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
@@ -525,6 +528,7 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
   ctx->cfg = *cfg;
   ctx->device = device;
   ctx->diag_skip_deint = opt.diag_skip_deint != 0;
+  ctx->adam_nt = opt.adam_nt;
   ctx->diag_shadow = opt.diag_shadow_deint;
   ctx->diag_shadow_at = opt.diag_shadow_at;
   hipError_t he = hipSetDevice(device);
@@ -1480,6 +1484,7 @@ static AdamArgs adam_args(const mvae_ctx* c) {
   a.lr1 = (c->cfg.lr[0] * std::sqrt(1.f - c->b2p[0])) / (1.f - c->b1p[0]);
   a.lr2 = (c->cfg.lr[1] * std::sqrt(1.f - c->b2p[1])) / (1.f - c->b1p[1]);
   a.tp = planes_of(c, c->theta);
+  a.nt = c->adam_nt;
   return a;
 }
 

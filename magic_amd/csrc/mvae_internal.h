@@ -269,6 +269,7 @@ struct AdamArgs {
   size_t n_all, n_enc; float lr1, lr2, b1, b2, eps;
   Planes tp;  // bf16 plane image of theta refreshed in the same pass (bf16 / f32x modes)
   size_t i0 = 0, i1 = ~size_t(0);  // the index range [i0, min(i1, n_all)) this launch updates
+  int nt = 0;  // moments and fp32 theta stored non-temporal (read again only by the next Adam)
 };
 hipError_t launch_adam(const AdamArgs& a, hipStream_t st);
 hipError_t launch_split_planes(const float* src, size_t n, const Planes& dst, hipStream_t st);

@@ -702,6 +702,12 @@ __global__ void latent_bwd_kernel(const float* __restrict__ ms, EpsSrc es,
 // opt1 (lr1, g1) over every trained variable, opt2 (lr2, g2) over the encoder slice;
 // both from the pre-step gradients: theta = (theta - d1) - d2.  lr_t precomputed on the
 // host in fp32 exactly as TF ApplyAdam (lr*sqrt(1-b2^t)/(1-b1^t) with fp32 beta powers).
+template <bool NT>
+__device__ __forceinline__ void st_f(float* p, float v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+template <bool NT>
 __global__ void adam_kernel(AdamArgs a) {
   const size_t i = a.i0 + (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= a.i1) return;
@@ -711,7 +717,7 @@ __global__ void adam_kernel(AdamArgs a) {
     float m = a.m1[i], v = a.v1[i];
     m += (g - m) * (1.f - a.b1);
     v += (g * g - v) * (1.f - a.b2);
-    a.m1[i] = m; a.v1[i] = v;
+    st_f<NT>(a.m1 + i, m); st_f<NT>(a.v1 + i, v);
     th -= (a.lr1 * m) / (sqrtf(v) + a.eps);
   }
   if (i < a.n_enc) {
@@ -719,10 +725,10 @@ __global__ void adam_kernel(AdamArgs a) {
     float m = a.m2[i], v = a.v2[i];
     m += (g - m) * (1.f - a.b1);
     v += (g * g - v) * (1.f - a.b2);
-    a.m2[i] = m; a.v2[i] = v;
+    st_f<NT>(a.m2 + i, m); st_f<NT>(a.v2 + i, v);
     th -= (a.lr2 * m) / (sqrtf(v) + a.eps);
   }
-  a.theta[i] = th;
+  st_f<NT>(a.theta + i, th);
   if (a.tp.p) planes_put(a.tp.p, a.tp.stride, a.tp.n, i, th);
 }
 
@@ -1067,7 +1073,8 @@ hipError_t launch_adam(const AdamArgs& a, hipStream_t st) {
   AdamArgs r = a;
   r.i1 = a.i1 < a.n_all ? a.i1 : a.n_all;
   if (r.i0 >= r.i1) return hipSuccess;
-  hipLaunchKernelGGL(adam_kernel, dim3(nblocks(r.i1 - r.i0, 256)), dim3(256), 0, st, r);
+  if (r.nt) hipLaunchKernelGGL(adam_kernel<true>, dim3(nblocks(r.i1 - r.i0, 256)), dim3(256), 0, st, r);
+  else hipLaunchKernelGGL(adam_kernel<false>, dim3(nblocks(r.i1 - r.i0, 256)), dim3(256), 0, st, r);
   return hipGetLastError();
 }
 
