@@ -40,7 +40,7 @@ struct DeintShape {
   static constexpr int NR = 64 / RPP;  // row passes per thread
   static_assert(NT % NO == 0 && 64 % RPP == 0, "whole rows per pass");
 };
-template <int PB, int NT>
+template <int PB, int NT, bool NTL = false>
 __device__ __forceinline__ void deint_load(const float4* __restrict__ x, int D, int bx, int by,
                                            float4 (&v)[DeintShape<PB, NT>::NR][6]) {
   using S = DeintShape<PB, NT>;
@@ -52,7 +52,15 @@ __device__ __forceinline__ void deint_load(const float4* __restrict__ x, int D, 
   for (int i = 0; i < S::NR; ++i) {
     const float4* src = x + ((size_t)(b0 + tid / S::NO + S::RPP * i) * 3 * D + 3 * (size_t)pix) / 4;
 #pragma unroll
-    for (int k = 0; k < 6; ++k) v[i][k] = src[k];
+    for (int k = 0; k < 6; ++k) {
+      if constexpr (NTL) {  // (read once: non-temporal)
+        typedef float f4 __attribute__((ext_vector_type(4)));
+        const f4 t = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src + k));
+        v[i][k] = make_float4(t.x, t.y, t.z, t.w);
+      } else {
+        v[i][k] = src[k];
+      }
+    }
   }
 }
 // one row's 8 pixels x 3 channels (interleaved, as X stores them) -> the byte of each block
@@ -172,13 +180,13 @@ __device__ __forceinline__ void deint_finish(int B, int D, int kts_f, int kts_w,
 }
 
 // the whole task (the standalone kernel's workgroup)
-template <int PB, int NT, int OS>
+template <int PB, int NT, int OS, bool NTL = false>
 __device__ __forceinline__ void deint_bits_task(const float4* __restrict__ x, int B, int D, int kts_f, int kts_w,
                                                 unsigned* __restrict__ xbf, unsigned* __restrict__ xbw,
                                                 unsigned char* __restrict__ xbits, int ldbits,
                                                 int* __restrict__ dyn, int bx, int by, DeintLds<PB, OS>& bt) {
   float4 v[DeintShape<PB, NT>::NR][6];
-  deint_load<PB, NT>(x, D, bx, by, v);
+  deint_load<PB, NT, NTL>(x, D, bx, by, v);
   deint_finish<PB, NT, OS, false>(B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, bx, by, v, bt, [] {}, [] {});
 }
 

@@ -137,6 +137,7 @@ struct mvae_ctx {
   // f0f the fused launch (bits path, its own split), f0fb the plane-path fallback that runs only
   // for a batch with a pixel other than 0 / 1; fuse_buf: the chunk counters, error word, order
   int adam_nt = 0;  // create option adam_nt
+  int deint_variant = 0;  // create option deint_variant
   bool fuse = false;
   GemmDesc f0f, f0fb;
   int* fuse_buf = nullptr;
@@ -463,6 +464,7 @@ struct CreateOpts {
   int deint_fuse = 0;   // ... the de-interleave run inside the layer-0 forward's launch (DeintJob)
   int deint_fuse_diag = 0;  // ... its timing diagnostics (DeintJob::diag; results invalid)
   int adam_nt = 1;      // Adam's moment / fp32 parameter stores non-temporal (C2 -0.6 %, C3 -0.3 %, r6za)
+  int deint_variant = 0;  // the bits de-interleave's form (launch_deint_bits; diagnostics / A-B)
   int conv2_nw = 8, conv2_tpb = 1, conv2_fpw = 2, conv2_wg = 8, conv2_half = 1, conv2_nchunk = 0;
 };
 
@@ -500,6 +502,7 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "deint_fuse" && in(0, 1)) o->deint_fuse = (int)v;
     else if (k == "deint_fuse_diag" && in(0, 31)) o->deint_fuse_diag = (int)v;
     else if (k == "adam_nt" && in(0, 1)) o->adam_nt = (int)v;
+    else if (k == "deint_variant" && in(0, 6)) o->deint_variant = (int)v;
     else if (k == "enc_chain_rows" && (v == 0 || (in(16, 96) && v % 16 == 0))) o->enc_chain_rows = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
     else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
@@ -529,6 +532,7 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
   ctx->device = device;
   ctx->diag_skip_deint = opt.diag_skip_deint != 0;
   ctx->adam_nt = opt.adam_nt;
+  ctx->deint_variant = opt.deint_variant;
   ctx->diag_shadow = opt.diag_shadow_deint;
   ctx->diag_shadow_at = opt.diag_shadow_at;
   hipError_t he = hipSetDevice(device);
@@ -1326,7 +1330,7 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
     int* cur = c->dyn ? (prev == c->dyn ? c->dyn + 1 : c->dyn) : nullptr;
     if (c->bits_on)  // the BitMats and target bits; the planes only for a batch not all 0 / 1
       MV_CHECK(launch_deint_bits(x, c->B, c->D, c->xbf, c->kts_f, c->xbw, c->kts_w, c->xbits, c->ldbits, cur,
-                                 prev, c->xs, planes_of(c, c->xs), c->ldx, c->x32dyn, st));
+                                 prev, c->xs, planes_of(c, c->xs), c->ldx, c->x32dyn, st, c->deint_variant));
     else
       MV_CHECK(launch_deinterleave(x, c->xs, planes_of(c, c->xs), cur, c->dyn ? prev : nullptr, c->B,
                                    c->D, c->ldx, c->x32mask, c->x32dyn, st, c->xbits, c->ldbits));
