@@ -1,12 +1,13 @@
 #!/bin/bash
-# r6zb: the de-interleave with non-temporal loads of X (deint variant 6) -- isolated and in-step
+# The current GPU session (overwritten per session; earlier sessions are in git history):
+#   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
+# r6zc: the final round-6 tree -- whole GPU suite, smoke, C2 timed-loop trace, default bench line
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-A="--no-cpu-baseline --pmc off --no-h2d --no-pipeline --no-configs --steps 60 --warmup 5"
+T="python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider"
+B="--no-cpu-baseline --pmc off --no-h2d --no-pipeline --no-configs --steps 20 --warmup 3 --mark-dominant"
+p() { echo "r6zc_prof_$1|240|cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/gpurun_out/prof_r6zc_$1 -o run -- python3 $PWD/bench.py --config $2 $B"; }
 bash tools/gpu_steps.sh \
-  "r6zb_deint|200|python tools/deint_bench.py --config C3 --variants 0,6,0,6 --rounds 3 && python tools/deint_bench.py --config C2 --variants 0,6 --rounds 3" \
-  "r6zb_c3_v0a|200|python bench.py --config C3 $A --create-opt deint_variant=0" \
-  "r6zb_c3_v6a|200|python bench.py --config C3 $A --create-opt deint_variant=6" \
-  "r6zb_c3_v0b|200|python bench.py --config C3 $A --create-opt deint_variant=0" \
-  "r6zb_c3_v6b|200|python bench.py --config C3 $A --create-opt deint_variant=6" \
-  "r6zb_c2_v0a|200|python bench.py --config C2 $A --create-opt deint_variant=0" \
-  "r6zb_c2_v6a|200|python bench.py --config C2 $A --create-opt deint_variant=6"
+  "r6zc_tests|800|$T -m gpu tests" \
+  "r6zc_smoke|240|python -c 'import __graft_entry__ as g; g.smoke()'" \
+  "$(p c2 C2)" "$(p c3 C3)" \
+  "r6zc_bench|900|python bench.py > gpurun_out/r6zc_bench.json"
