@@ -773,6 +773,7 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   p.abits = d.Abits; p.abits_kts = d.abits_kts; p.abits_sb = d.abits_sb; p.anb = d.anb;
   p.dj = d.dj;
   p.bits_reg = d.bits_reg;
+  p.prio = d.prio;
   // the fused de-interleave rides on the eight-phase kernel's bits path only
   if (d.dj.nworkers && (g.tn != TN_E8 || !d.Abits || d.at || d.bt || (epi != EPI_STORE && epi != EPI_ACT)))
     return hipErrorInvalidValue;

@@ -330,12 +330,14 @@ struct E8 {
       fb[3] = rd_tr<O + 8192>(aB[1]);
     }
   }
-  // the quadrant's 16 MFMAs once this wave's reads have landed
+  // the quadrant's 16 MFMAs once this wave's reads have landed (priority 1 around them unless
+  // flips is false: PParams::prio)
+  bool flips = true;
   template <int MS, int NS>
   __device__ __forceinline__ void mfma_q(const bf16x8 (&fa)[8], const bf16x8 (&fb)[4]) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_setprio(1);
+    if (flips) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kh = 0; kh < 2; ++kh)
 #pragma unroll
@@ -344,7 +346,7 @@ struct E8 {
         for (int nb = 0; nb < 2; ++nb)
           acc[2 * MS + (mb >> 1)][mb & 1][NS][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
               fa[2 * mb + kh], fb[2 * nb + kh], acc[2 * MS + (mb >> 1)][mb & 1][NS][nb], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if (flips) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_sched_barrier(0);
   }
   template <int H, int Bf>
@@ -511,6 +513,11 @@ __device__ __forceinline__ void e8_tile(const PParams& pp, short* smem) {
   // waves 4-7 (the second wave of every SIMD), as a scalar condition: s_barrier ignores EXEC
   // (stamped builds, diag 128: no stagger -- both halves in the same phase)
   const bool lag = __builtin_amdgcn_readfirstlane(wave) >= 4 && !(ST && (pp.diag & 128));
+  // priority (PParams::prio): 0 priority 1 around every MFMA quadrant; 1 priority 1 for the
+  // lagging half (waves 4-7) for the whole loop, no flips (cdna_hip_programming.md T5, static
+  // form); 2 no priorities
+  s.flips = pp.prio == 0;
+  if (pp.prio == 1 && lag) __builtin_amdgcn_s_setprio(1);
 
   if (total > 0) {
     // The (k-tile, pair) walk. Default: pairs innermost. reuse (f32x plane pairs): k-tiles in

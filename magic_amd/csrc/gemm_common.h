@@ -53,6 +53,7 @@ struct PParams {
   int npairs_a0 = 1;                // the leading pairs with A plane 0 (the bits path's pairs)
   DeintJob dj;                      // eight-phase kernel: the fused de-interleave (GemmDesc::dj)
   int bits_reg = 0;                 // eight-phase bits path: A words by loads to registers (E8 BITS 2)
+  int prio = 0;                     // eight-phase kernel: s_setprio form (gemm_bf16e.hip e8_tile)
 };
 
 // tanh as an odd [13/6] rational in x on [-7.905, 7.905] (clamped beyond, where tanh rounds to

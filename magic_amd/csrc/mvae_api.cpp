@@ -138,6 +138,7 @@ struct mvae_ctx {
   // for a batch with a pixel other than 0 / 1; fuse_buf: the chunk counters, error word, order
   int adam_nt = 0;  // create option adam_nt
   int deint_variant = 0;  // create option deint_variant
+  int e8_prio = 0;        // create option e8_prio (PParams::prio)
   bool fuse = false;
   GemmDesc f0f, f0fb;
   int* fuse_buf = nullptr;
@@ -465,6 +466,7 @@ struct CreateOpts {
   int deint_fuse_diag = 0;  // ... its timing diagnostics (DeintJob::diag; results invalid)
   int adam_nt = 1;      // Adam's moment / fp32 parameter stores non-temporal (C2 -0.6 %, C3 -0.3 %, r6za)
   int deint_variant = 0;  // the bits de-interleave's form (launch_deint_bits; diagnostics / A-B)
+  int e8_prio = 0;      // the eight-phase kernel's s_setprio form (PParams::prio; A-B)
   int conv2_nw = 8, conv2_tpb = 1, conv2_fpw = 2, conv2_wg = 8, conv2_half = 1, conv2_nchunk = 0;
 };
 
@@ -503,6 +505,7 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "deint_fuse_diag" && in(0, 31)) o->deint_fuse_diag = (int)v;
     else if (k == "adam_nt" && in(0, 1)) o->adam_nt = (int)v;
     else if (k == "deint_variant" && in(0, 6)) o->deint_variant = (int)v;
+    else if (k == "e8_prio" && in(0, 2)) o->e8_prio = (int)v;
     else if (k == "enc_chain_rows" && (v == 0 || (in(16, 96) && v % 16 == 0))) o->enc_chain_rows = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
     else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
@@ -533,6 +536,7 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
   ctx->diag_skip_deint = opt.diag_skip_deint != 0;
   ctx->adam_nt = opt.adam_nt;
   ctx->deint_variant = opt.deint_variant;
+  ctx->e8_prio = opt.e8_prio;
   ctx->diag_shadow = opt.diag_shadow_deint;
   ctx->diag_shadow_at = opt.diag_shadow_at;
   hipError_t he = hipSetDevice(device);
@@ -1257,6 +1261,13 @@ static int run(mvae_ctx* ctx, const GemmDesc& d, hipStream_t st, int r = -1) {
     if (dd.epi.xdyn == ctx->dyn) dd.epi.xdyn = ctx->dyn_cur;
     if (dd.epi.xnb == ctx->dyn + 2) dd.epi.xnb = ctx->dyn_cur + 2;
     if (dd.anb == ctx->dyn + 2) dd.anb = ctx->dyn_cur + 2;
+    dd.prio = ctx->e8_prio;
+    MV_CHECK(gemm_run(dd, ws, ctx->ws_elems, st));
+    return MVAE_OK;
+  }
+  if (ctx->e8_prio) {
+    GemmDesc dd = d;
+    dd.prio = ctx->e8_prio;
     MV_CHECK(gemm_run(dd, ws, ctx->ws_elems, st));
     return MVAE_OK;
   }

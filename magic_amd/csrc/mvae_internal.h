@@ -135,6 +135,7 @@ struct GemmDesc {
   const int* anb = nullptr;
   DeintJob dj;                         // the fused de-interleave (eight-phase bits path only)
   int bits_reg = 0;                    // bits path: A words by loads to registers (gemm_bf16e.hip E8)
+  int prio = 0;                        // eight-phase kernel: s_setprio form (PParams::prio)
   GemmEpi epi;
 };
 

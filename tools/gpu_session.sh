@@ -1,13 +1,16 @@
 #!/bin/bash
-# The current GPU session (overwritten per session; earlier sessions are in git history):
-#   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r6zc: the final round-6 tree -- whole GPU suite, smoke, C2 timed-loop trace, default bench line
+# r6zd: the eight-phase kernel's s_setprio form (e8_prio: 0 flips around every MFMA quadrant,
+# 1 static priority for the lagging half, 2 none), same box, alternating
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-T="python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider"
-B="--no-cpu-baseline --pmc off --no-h2d --no-pipeline --no-configs --steps 20 --warmup 3 --mark-dominant"
-p() { echo "r6zc_prof_$1|240|cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/gpurun_out/prof_r6zc_$1 -o run -- python3 $PWD/bench.py --config $2 $B"; }
+A="--no-cpu-baseline --pmc off --no-h2d --no-pipeline --no-configs --steps 60 --warmup 5"
 bash tools/gpu_steps.sh \
-  "r6zc_tests|800|$T -m gpu tests" \
-  "r6zc_smoke|240|python -c 'import __graft_entry__ as g; g.smoke()'" \
-  "$(p c2 C2)" "$(p c3 C3)" \
-  "r6zc_bench|900|python bench.py > gpurun_out/r6zc_bench.json"
+  "r6zd_c3_p0a|200|python bench.py --config C3 $A --create-opt e8_prio=0" \
+  "r6zd_c3_p1a|200|python bench.py --config C3 $A --create-opt e8_prio=1" \
+  "r6zd_c3_p2a|200|python bench.py --config C3 $A --create-opt e8_prio=2" \
+  "r6zd_c3_p0b|200|python bench.py --config C3 $A --create-opt e8_prio=0" \
+  "r6zd_c3_p1b|200|python bench.py --config C3 $A --create-opt e8_prio=1" \
+  "r6zd_c3_p2b|200|python bench.py --config C3 $A --create-opt e8_prio=2" \
+  "r6zd_c2_p0a|200|python bench.py --config C2 $A --create-opt e8_prio=0" \
+  "r6zd_c2_p1a|200|python bench.py --config C2 $A --create-opt e8_prio=1" \
+  "r6zd_c2_p0b|200|python bench.py --config C2 $A --create-opt e8_prio=0" \
+  "r6zd_c2_p1b|200|python bench.py --config C2 $A --create-opt e8_prio=1"
