@@ -88,7 +88,7 @@ __device__ __forceinline__ bool deint_octet(const float (&e)[24], unsigned (&by3
 // (lane & 15), k-octet 8 kk + 4 kh + (lane >> 4); one 16-B store, SC1 written through), the
 // weight-gradient words one at a time (pixel 64 kk + 16 (2 j + h) + (lane & 15), rows 32 kh +
 // 8 (lane >> 4) + 0..7: bit (pixel & 7) of 8 row bytes of one octet)
-template <int PB, int OS, bool SC1>
+template <int PB, int OS, bool SC1, bool NOW = false>
 __device__ __forceinline__ void deint_words(int t0, int nt, int B, int D, int kts_f, int kts_w,
                                             unsigned* __restrict__ xbf, unsigned* __restrict__ xbw, int bx,
                                             int by, const DeintLds<PB, OS>& bt) {
@@ -119,7 +119,7 @@ __device__ __forceinline__ void deint_words(int t0, int nt, int B, int D, int kt
       *reinterpret_cast<uint4*>(dst) = make_uint4(w4[0], w4[1], w4[2], w4[3]);
     }
   }
-  for (int wi = t0; wi < 3 * PB * 128; wi += nt) {
+  for (int wi = t0; wi < (NOW ? 0 : 3 * PB * 128); wi += nt) {  // (NOW: diagnostics, no xbw)
     const int c = wi / (PB * 128), kk = (wi / 128) % PB, wl = wi & 127, lane = wl >> 1, j = wl & 1;
     const int grow = c * B + b0;
     const int pq = p0 + 64 * kk;
@@ -140,7 +140,7 @@ __device__ __forceinline__ void deint_words(int t0, int nt, int B, int D, int kt
   }
 }
 
-template <int PB, int NT, int OS, bool SC1, class FW, class FS>
+template <int PB, int NT, int OS, bool SC1, class FW, class FS, bool NOW = false>
 __device__ __forceinline__ void deint_finish(int B, int D, int kts_f, int kts_w, unsigned* __restrict__ xbf,
                                              unsigned* __restrict__ xbw, unsigned char* __restrict__ xbits,
                                              int ldbits, int* __restrict__ dyn, int bx, int by,
@@ -176,18 +176,20 @@ __device__ __forceinline__ void deint_finish(int B, int D, int kts_f, int kts_w,
   }
   __syncthreads();
   synced();
-  deint_words<PB, OS, SC1>(tid, NT, B, D, kts_f, kts_w, xbf, xbw, bx, by, bt);
+  deint_words<PB, OS, SC1, NOW>(tid, NT, B, D, kts_f, kts_w, xbf, xbw, bx, by, bt);
 }
 
 // the whole task (the standalone kernel's workgroup)
-template <int PB, int NT, int OS, bool NTL = false>
+template <int PB, int NT, int OS, bool NTL = false, bool NOW = false>
 __device__ __forceinline__ void deint_bits_task(const float4* __restrict__ x, int B, int D, int kts_f, int kts_w,
                                                 unsigned* __restrict__ xbf, unsigned* __restrict__ xbw,
                                                 unsigned char* __restrict__ xbits, int ldbits,
                                                 int* __restrict__ dyn, int bx, int by, DeintLds<PB, OS>& bt) {
   float4 v[DeintShape<PB, NT>::NR][6];
   deint_load<PB, NT, NTL>(x, D, bx, by, v);
-  deint_finish<PB, NT, OS, false>(B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, bx, by, v, bt, [] {}, [] {});
+  auto none = [] {};
+  deint_finish<PB, NT, OS, false, decltype(none)&, decltype(none)&, NOW>(B, D, kts_f, kts_w, xbf, xbw, xbits,
+                                                                         ldbits, dyn, bx, by, v, bt, none, none);
 }
 
 }  // namespace mvae

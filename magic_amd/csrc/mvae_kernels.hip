@@ -841,7 +841,7 @@ __global__ __launch_bounds__(256) void make_batch4_kernel(const unsigned char* _
 // The layer-0 pixel operand of a 0/1 batch as BitMats (deint_bits.h): one workgroup per task of
 // 64 batch rows x 64 PB pixels. Raises the not-binary word (*dyn slot 2) when a pixel is neither 0
 // nor 1: the step then runs deint_grey_kernel (the planes) and the GEMMs read the planes.
-template <int PB, int NT, int OS, bool NTL = false>
+template <int PB, int NT, int OS, bool NTL = false, bool NOW = false>
 __global__ __launch_bounds__(NT) void deint_bits_kernel(const float4* __restrict__ x, int B, int D, int kts_f,
                                                         int kts_w, unsigned* __restrict__ xbf,
                                                         unsigned* __restrict__ xbw,
@@ -849,7 +849,7 @@ __global__ __launch_bounds__(NT) void deint_bits_kernel(const float4* __restrict
                                                         int* __restrict__ dyn, int* __restrict__ dyn_next) {
   if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) dyn_next[0] = dyn_next[2] = 0;
   __shared__ __attribute__((aligned(16))) DeintLds<PB, OS> bt;
-  deint_bits_task<PB, NT, OS, NTL>(x, B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, blockIdx.x, blockIdx.y, bt);
+  deint_bits_task<PB, NT, OS, NTL, NOW>(x, B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, blockIdx.x, blockIdx.y, bt);
 }
 
 // The plane image of a batch with a pixel other than 0 or 1 (after deint_bits_kernel raised the
@@ -947,6 +947,10 @@ hipError_t launch_deint_bits(const float* x, int B, int D, unsigned* xbf, int kt
       if (e != hipSuccess) return e;
       break;
     }
+    case 7:  // (diagnostics) the step's form without the weight-gradient words
+      hipLaunchKernelGGL((deint_bits_kernel<2, 256, 72, false, true>), dim3((kts_f + 1) / 2, B / 64), dim3(256), 0, st,
+                         x4, B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
+      break;
     case 6:  // the step's form with non-temporal loads of X (2x slower: r6zb_deint_nt_loads.txt)
       hipLaunchKernelGGL((deint_bits_kernel<2, 256, 72, true>), dim3((kts_f + 1) / 2, B / 64), dim3(256), 0, st, x4, B,
                          D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
