@@ -139,6 +139,12 @@ struct mvae_ctx {
   int adam_nt = 0;  // create option adam_nt
   int deint_variant = 0;  // create option deint_variant
   int e8_prio = 0;        // create option e8_prio (PParams::prio)
+  // create option xbw_split: the de-interleave writes the forward BitMat only and the weight
+  // gradient's (xbw) is transposed from it on the side stream (launch_bits_transpose), joined by
+  // xbw_ev before the layer-0 weight gradient
+  int xbw_split = 0;
+  hipEvent_t xbw_ev = nullptr;
+  bool xbw_pending = false;
   bool fuse = false;
   GemmDesc f0f, f0fb;
   int* fuse_buf = nullptr;
@@ -433,6 +439,7 @@ int mvae_destroy(mvae_ctx* ctx) {
   for (auto& pd : ctx->pending) { hipEventDestroy(pd.a); hipEventDestroy(pd.b); }
   for (auto e : ctx->event_pool) hipEventDestroy(e);
   for (auto e : ctx->sync_ev) hipEventDestroy(e);
+  if (ctx->xbw_ev) hipEventDestroy(ctx->xbw_ev);
   if (ctx->side) hipStreamDestroy(ctx->side);
   if (ctx->stage) hipStreamDestroy(ctx->stage);
   for (void* p : ctx->allocs) hipFree(p);
@@ -467,6 +474,9 @@ struct CreateOpts {
   int adam_nt = 1;      // Adam's moment / fp32 parameter stores non-temporal (C2 -0.6 %, C3 -0.3 %, r6za)
   int deint_variant = 0;  // the bits de-interleave's form (launch_deint_bits; diagnostics / A-B)
   int e8_prio = 0;      // the eight-phase kernel's s_setprio form (PParams::prio; A-B)
+  int xbw_split = 2;    // the weight gradient's BitMat transposed from the forward's (mvae_ctx):
+                        // 0 off, 1 on, 2 where the layer-0 forward's workgroups leave >= 32 CUs
+                        // (C3 -0.6 %, C5 -0.4 %; C2, 480 forward workgroups: +3.8 % on, r6zf)
   int conv2_nw = 8, conv2_tpb = 1, conv2_fpw = 2, conv2_wg = 8, conv2_half = 1, conv2_nchunk = 0;
 };
 
@@ -506,6 +516,7 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "adam_nt" && in(0, 1)) o->adam_nt = (int)v;
     else if (k == "deint_variant" && in(0, 6)) o->deint_variant = (int)v;
     else if (k == "e8_prio" && in(0, 2)) o->e8_prio = (int)v;
+    else if (k == "xbw_split" && in(0, 2)) o->xbw_split = (int)v;
     else if (k == "enc_chain_rows" && (v == 0 || (in(16, 96) && v % 16 == 0))) o->enc_chain_rows = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
     else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
@@ -537,6 +548,7 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
   ctx->adam_nt = opt.adam_nt;
   ctx->deint_variant = opt.deint_variant;
   ctx->e8_prio = opt.e8_prio;
+  ctx->xbw_split = opt.xbw_split == 1 ? 1 : 0;  // (2: decided with the forward's plan, below)
   ctx->diag_shadow = opt.diag_shadow_deint;
   ctx->diag_shadow_at = opt.diag_shadow_at;
   hipError_t he = hipSetDevice(device);
@@ -988,6 +1000,15 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
     }
   no_fuse:;
   }
+  if (opt.xbw_split == 2 && c->bits_on && !c->fuse) {  // the forward's workgroups leave CUs free?
+    const GemmDesc& f0 = c->fwd_enc[0];
+    int sp = 0, tn = 0, tm = 0;
+    gemm_bf16_wide_plan(f0, ~size_t(0), &sp, &tn, &tm);
+    const long long tiles = (long long)((f0.M + tm - 1) / tm) * ((f0.N + (tn == GEMM_TN_E8 ? 256 : tn) - 1) /
+                                                                   (tn == GEMM_TN_E8 ? 256 : tn)) * f0.batch;
+    c->xbw_split = tiles * sp <= 224 ? 1 : 0;
+  }
+  if (c->fuse) c->xbw_split = 0;  // (the fused launch's workers write xbw themselves)
   size_t ws = 0;
   auto wsz = [&](const GemmDesc& d) { ws = std::max(ws, gemm_workspace_elems(d)); };
   if (c->fuse) wsz(c->f0f);
@@ -1073,6 +1094,7 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
       if (se == hipSuccess) se = hipMalloc(&q, (size_t)3 * c->B * c->ldx * sizeof(unsigned short));
       if (se == hipSuccess) { c->allocs.push_back(q); c->shadow = static_cast<unsigned short*>(q); }
     }
+    if (se == hipSuccess) se = hipEventCreateWithFlags(&c->xbw_ev, hipEventDisableTiming);
     for (int i = 0; se == hipSuccess && i < 16; ++i) {
       hipEvent_t ev = nullptr;
       // stream-to-stream ordering on this device only: no system-scope fence. The producer side
@@ -1300,6 +1322,10 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
     MV_CHECK(hipEventRecord(c->sync_ev[c->sync_next % c->sync_ev.size()], c->side));
     MV_CHECK(hipStreamWaitEvent(st, c->sync_ev[c->sync_next++ % c->sync_ev.size()], 0));
   }
+  if (c->xbw_pending) {  // the last transpose read the forward BitMat this pass rewrites
+    c->xbw_pending = false;
+    MV_CHECK(hipStreamWaitEvent(st, c->xbw_ev, 0));
+  }
   if (c->stage_pending) {  // (diagnostics) the last shadow pass ends before this step
     c->stage_pending = false;
     MV_CHECK(hipEventRecord(c->sync_ev[c->sync_next % c->sync_ev.size()], c->stage));
@@ -1339,9 +1365,21 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
     // the previous one (its readers are all behind on this stream), no memset launch per step
     int* prev = c->dyn_cur ? c->dyn_cur : c->dyn;
     int* cur = c->dyn ? (prev == c->dyn ? c->dyn + 1 : c->dyn) : nullptr;
-    if (c->bits_on)  // the BitMats and target bits; the planes only for a batch not all 0 / 1
+    if (c->bits_on) {  // the BitMats and target bits; the planes only for a batch not all 0 / 1
+      const bool split = c->xbw_split && draw == ENC_TRAIN;  // (eval passes need no xbw)
       MV_CHECK(launch_deint_bits(x, c->B, c->D, c->xbf, c->kts_f, c->xbw, c->kts_w, c->xbits, c->ldbits, cur,
-                                 prev, c->xs, planes_of(c, c->xs), c->ldx, c->x32dyn, st, c->deint_variant));
+                                 prev, c->xs, planes_of(c, c->xs), c->ldx, c->x32dyn, st,
+                                 split ? 7 : c->deint_variant));
+      if (split) {  // xbw from xbf on the side stream, beside the layer-0 forward
+        const bool two = c->use_side && c->side;
+        hipStream_t sd = two ? c->side : st;
+        if (two)
+          if (int rc = stream_wait(c, st, sd)) return rc;
+        MV_CHECK(launch_bits_transpose(c->xbf, c->kts_f, c->xbw, c->kts_w, c->B, sd));
+        MV_CHECK(hipEventRecord(c->xbw_ev, sd));
+        c->xbw_pending = true;
+      }
+    }
     else
       MV_CHECK(launch_deinterleave(x, c->xs, planes_of(c, c->xs), cur, c->dyn ? prev : nullptr, c->B,
                                    c->D, c->ldx, c->x32mask, c->x32dyn, st, c->xbits, c->ldbits));
@@ -1521,6 +1559,10 @@ static int backward_part(mvae_ctx* ctx, int part, hipStream_t st, bool join_dec)
   };
   const int n = c->nenc;
   auto w0chunk = [&](int r) -> int {  // layer-0 weight gradient, chunk r of R
+    if (c->xbw_pending) {  // its BitMat, transposed on the side stream (xbw_split)
+      c->xbw_pending = false;
+      MV_CHECK(hipStreamWaitEvent(st, c->xbw_ev, 0));
+    }
     const GemmDesc& d = R == 1 ? c->bwd_enc[n] : c->w0c[c->w0_chunks][r];
     return run(c, d, st, c->bwd_enc_r[n]);
   };

@@ -226,6 +226,9 @@ hipError_t launch_deinterleave(const float* x, float* xs, const Planes& xp, int*
 // (a gated second kernel) the planes of xp, the fp32 rows of f32dyn_mask and the inexact flag as
 // launch_deinterleave writes them. dyn_next: the other flag slot, zeroed. Both BitMats must be
 // zero-filled once (their padding is never written).
+// the weight gradient's BitMat xbw from the forward's xbf (both of a 3B-row batch; see
+// bits_transpose_kernel)
+hipError_t launch_bits_transpose(const unsigned* xbf, int kts_f, unsigned* xbw, int kts_w, int B, hipStream_t st);
 // the grey pass alone (after a fused launch: also zeroes its chunk counters done[0 .. ndone))
 hipError_t launch_deint_grey(const float* x, int B, int D, int* dyn, float* xs, const Planes& xp, int ldx,
                              int f32dyn_mask, int* done, int ndone, hipStream_t st);

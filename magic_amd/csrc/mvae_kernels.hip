@@ -852,6 +852,59 @@ __global__ __launch_bounds__(NT) void deint_bits_kernel(const float4* __restrict
   deint_bits_task<PB, NT, OS, NTL, NOW>(x, B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, blockIdx.x, blockIdx.y, bt);
 }
 
+// The weight gradient's BitMat (pixels x stacked rows) from the forward's (stacked rows x
+// pixels): one wave per 64 x 64 bit tile -- a quarter of a block on either side -- its 128 words in,
+// the tile as [8 pixel octets][64 rows] bytes in LDS, its 128 transposed words out (the 8 x 8 bit
+// transpose of deint_bits.h). The de-interleave then writes only the forward words (deint
+// variant 7): the transpose runs on the side stream beside the layer-0 forward, whose 192 tiles
+// (C3) leave CUs free, and the layer-0 weight gradient waits for it.
+__device__ __forceinline__ unsigned bits_compact(unsigned s) {  // inverse of bits_spread (low byte)
+  unsigned e = s & 0xFu, o = (s >> 16) & 0xFu;
+  e = (e | (e << 2)) & 0x33u; e = (e | (e << 1)) & 0x55u;
+  o = (o | (o << 2)) & 0x33u; o = (o | (o << 1)) & 0x55u;
+  return e | (o << 1);
+}
+__global__ __launch_bounds__(256) void bits_transpose_kernel(const unsigned* __restrict__ xbf, int kts_f,
+                                                             unsigned* __restrict__ xbw, int kts_w, int nrow64) {
+  __shared__ __attribute__((aligned(16))) unsigned char tb[4][8][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int tile = blockIdx.x * 4 + wave;
+  const bool ok = tile < nrow64 * kts_f;
+  const int a = ok ? tile % nrow64 : 0, b = ok ? tile / nrow64 : 0;  // stacked-row tile, pixel tile
+  if (ok) {
+    const uint2 w = *reinterpret_cast<const uint2*>(xbf + ((size_t)(a >> 2) * kts_f + b) * BITMAT_BLOCK_WORDS +
+                                                    (a & 3) * 128 + 2 * lane);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int kh = 0; kh < 2; ++kh)
+          tb[wave][4 * kh + (lane >> 4)][16 * (2 * j + h) + (lane & 15)] =
+              (unsigned char)bits_compact((j ? w.y : w.x) >> (8 * h + 4 * kh));
+  }
+  __syncthreads();
+  if (!ok) return;
+  unsigned out[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    unsigned wo = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int kh = 0; kh < 2; ++kh) {
+        const int p = 16 * (2 * j + h) + (lane & 15);
+        const unsigned long long rows =
+            *reinterpret_cast<const unsigned long long*>(&tb[wave][p >> 3][32 * kh + 8 * (lane >> 4)]);
+        const unsigned long long col = (rows >> (p & 7)) & 0x0101010101010101ull;
+        wo |= bits_spread((unsigned)((col * 0x0102040810204080ull) >> 56)) << (8 * h + 4 * kh);
+      }
+    out[j] = wo;
+  }
+  *reinterpret_cast<uint2*>(xbw + ((size_t)(b >> 2) * kts_w + a) * BITMAT_BLOCK_WORDS + (b & 3) * 128 + 2 * lane) =
+      make_uint2(out[0], out[1]);
+}
+
 // The plane image of a batch with a pixel other than 0 or 1 (after deint_bits_kernel raised the
 // not-binary word; else every workgroup returns at once): bf16 plane 0 (planes 1-2 of the exact
 // split too when np == 3), the fp32 rows of the blocks in f32mask, and the inexact flag (*dyn) --
@@ -947,7 +1000,7 @@ hipError_t launch_deint_bits(const float* x, int B, int D, unsigned* xbf, int kt
       if (e != hipSuccess) return e;
       break;
     }
-    case 7:  // (diagnostics) the step's form without the weight-gradient words
+    case 7:  // the step's form without the weight-gradient words (launch_bits_transpose writes them)
       hipLaunchKernelGGL((deint_bits_kernel<2, 256, 72, false, true>), dim3((kts_f + 1) / 2, B / 64), dim3(256), 0, st,
                          x4, B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
       break;
@@ -976,6 +1029,15 @@ hipError_t launch_deint_bits(const float* x, int B, int D, unsigned* xbf, int kt
                          kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
   }
   return launch_deint_grey(x, B, D, dyn, xs, xp, ldx, f32dyn_mask, nullptr, 0, st);
+}
+
+hipError_t launch_bits_transpose(const unsigned* xbf, int kts_f, unsigned* xbw, int kts_w, int B, hipStream_t st) {
+  if (B % 64 || kts_f <= 0 || kts_w != bitmat_kts(3 * B)) return hipErrorInvalidValue;
+  const int nrow64 = 3 * B / 64;
+  const long long tiles = (long long)nrow64 * kts_f;
+  hipLaunchKernelGGL(bits_transpose_kernel, dim3((unsigned)((tiles + 3) / 4)), dim3(256), 0, st, xbf, kts_f, xbw,
+                     kts_w, nrow64);
+  return hipGetLastError();
 }
 
 hipError_t launch_deint_grey(const float* x, int B, int D, int* dyn, float* xs, const Planes& xp, int ldx,

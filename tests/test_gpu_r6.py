@@ -169,3 +169,40 @@ def test_deint_fuse_small_step_vs_oracle(prec, grey):
         check_step(cfg, grey=grey, recon=True)
     else:
         check_step(cfg, grey=grey, tol=5e-2, loss_tol=2e-3, dist_tol=2e-2, recon=True)
+
+
+# ------------------------------------------------------------------ xbw transposed from xbf
+
+@pytest.mark.parametrize("case", ["C3", "C2", "small"])
+def test_xbw_split_steps_bitwise(case):
+    """Option xbw_split: the de-interleave writes the forward BitMat only and the layer-0 weight
+    gradient's BitMat is transposed from it on the side stream (bits_transpose_kernel), joined
+    before the weight gradient. The same bits, so three training steps (the second batch grey:
+    the planes path) leave bitwise identical parameters and losses -- at C3 (bf16), C2 (f32x) and a
+    ragged small shape (D = 400: a partial last pixel tile; B = 320)."""
+    from magic_amd.config import baseline_config, preset
+    from magic_amd.engine import Engine
+    from tests.gpu_helpers import make_params
+    if case == "small":
+        cfg = preset("8c", image_size=20, batch=320, precision="bf16").replace(enc=(300, 260, 280))
+    else:
+        cfg = baseline_config(case)
+    P = make_params(cfg)
+    batches = _batches(cfg, 3, 1, 11)
+    res = []
+    for split in (0, 1):
+        eng = Engine(cfg.replace(options=f"xbw_split={split}"), 0)
+        try:
+            eng.load_params(P)
+            L = []
+            for x, a in batches:
+                eng.train_step(x, a)
+                L.append(eng.losses.clone())
+            torch.cuda.synchronize()
+            res.append(({k: v.cpu() for k, v in eng.params().items()}, torch.stack(L).cpu()))
+        finally:
+            eng.close()
+    (p0, l0), (p1, l1) = res
+    assert torch.equal(l0, l1), (l0, l1)
+    for k in p0:
+        assert torch.equal(p0[k], p1[k]), k
