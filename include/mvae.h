@@ -135,7 +135,11 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out);
  * registers; a batch with another pixel value takes the planes; default 1), bits_reg (0/1: each
  * wave loads its A words straight to registers, else through an LDS copy of the block; default
  * 1), deint_fuse (0/1: the de-interleave's workers inside the layer-0 forward's launch beside its
- * tiles, handing chunks over by counters; measured slower, default 0). Diagnostics, results
+ * tiles, handing chunks over by counters; measured slower, default 0), xbw_split (0/1/2: the
+ * weight gradient's BitMat transposed from the forward's on the side stream instead of written by
+ * the de-interleave; 2 = where the layer-0 forward leaves CUs idle, default), adam_nt (0/1: Adam's
+ * moments and fp32 parameters stored non-temporal, default 1), e8_prio (0-2, A/B: the eight-phase
+ * kernel's s_setprio form, default 0), deint_variant (0-7, A/B: the de-interleave's form). Diagnostics, results
  * meaningless: deint_fuse_diag (0-31: parts of the fused launch switched off), diag_skip_deint (1: de-interleave only the first batch -- a timing bound),
  * diag_shadow_deint (-1 or a workgroup count > 0: a second de-interleave of each step's input
  * into a scratch image on a low-priority stream, launched at diag_shadow_at = 0 the forward,
