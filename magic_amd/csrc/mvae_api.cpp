@@ -77,6 +77,7 @@ struct mvae_ctx {
   float *ms = nullptr, *z = nullptr, *a1 = nullptr, *a2 = nullptr, *du = nullptr;
   float *rowpart = nullptr, *rowvals = nullptr, *dist = nullptr, *draw = nullptr, *losses = nullptr;
   float *colsq = nullptr, *coldot = nullptr, *cspart = nullptr, *eps = nullptr;
+  int* cscnt = nullptr;  // create option cs_one: the column statistics' per-column-block counters
   float* rowfwd = nullptr;   // [B][4] latent forward row sums (KL, deformation, sq-diff distance)
   LatentEps le;              // eps of the last forward (buffer, or the Philox call regenerated)
   bool eps_lazy = false;     // le is a Philox call whose values the eps buffer does not hold yet
@@ -474,6 +475,8 @@ struct CreateOpts {
   int adam_nt = 1;      // Adam's moment / fp32 parameter stores non-temporal (C2 -0.6 %, C3 -0.3 %, r6za)
   int deint_variant = 0;  // the bits de-interleave's form (launch_deint_bits; diagnostics / A-B)
   int e8_prio = 0;      // the eight-phase kernel's s_setprio form (PParams::prio; A-B)
+  int cs_one = 1;       // the column statistics in one launch (the last chunk's workgroup sums the
+                        // partials in colstats_final_kernel's order: the same bits)
   int xbw_split = 2;    // the weight gradient's BitMat transposed from the forward's (mvae_ctx):
                         // 0 off, 1 on, 2 where the layer-0 forward's workgroups leave >= 32 CUs
                         // (C3 -0.6 %, C5 -0.4 %; C2, 480 forward workgroups: +3.8 % on, r6zf)
@@ -517,6 +520,7 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "deint_variant" && in(0, 6)) o->deint_variant = (int)v;
     else if (k == "e8_prio" && in(0, 2)) o->e8_prio = (int)v;
     else if (k == "xbw_split" && in(0, 2)) o->xbw_split = (int)v;
+    else if (k == "cs_one" && in(0, 1)) o->cs_one = (int)v;
     else if (k == "enc_chain_rows" && (v == 0 || (in(16, 96) && v % 16 == 0))) o->enc_chain_rows = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
     else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
@@ -640,6 +644,7 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
   ALLOC(c->colsq, 2 * L);
   ALLOC(c->coldot, L);
   ALLOC(c->cspart, (size_t)c->nchunk * 2 * L);
+  if (opt.cs_one) ALLOC(*reinterpret_cast<float**>(&c->cscnt), (2 * L + 63) / 64);  // (zeroed)
   ALLOC(c->eps, 3 * B * L);
   ALLOC(c->rowfwd, 4 * B);
   ALLOC(c->dzd2, B * c->ld_d2);
@@ -1445,7 +1450,7 @@ static int encode(mvae_ctx* ctx, const float* x, const float* eps, hipStream_t s
   if (c->cfg.metric == MVAE_METRIC_COSINE) {
     TIMED("colsq");
     MV_CHECK(launch_colstats(0, c->z, c->B, c->L, c->ldz, nullptr, nullptr, c->cspart, c->nchunk,
-                             c->colsq, st));
+                             c->colsq, st, c->cscnt));
   }
   return MVAE_OK;
 }
@@ -1492,7 +1497,7 @@ extern "C" int mvae_metric(mvae_ctx* ctx, const float* areas, void* stream) {
   if (c->cfg.metric == MVAE_METRIC_COSINE) {
     TIMED("coldot");
     MV_CHECK(launch_colstats(1, c->z, c->B, c->L, c->ldz, c->colsq, c->draw, c->cspart, c->nchunk,
-                             c->coldot, st));
+                             c->coldot, st, c->cscnt));
   }
   ctx->phase = 2;
   return MVAE_OK;

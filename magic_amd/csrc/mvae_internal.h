@@ -256,9 +256,11 @@ struct LatentEps {
 // rowfwd[b] = {sum KL term, sum (z_lock - z_rot)^2, sum (z_lock - z_key)^2, 0}.
 hipError_t launch_latent_fwd(const float* ms, const LatentEps& eps, float* z, const Planes& zp,
                              int zmask, int B, int L, int ldz, float* rowfwd, hipStream_t st);
-// out[j] for j in [0, ncols): mode 0 = colsq (z_lock^2 | z_key^2), mode 1 = coldot.
+// out[j] for j in [0, ncols): mode 0 = colsq (z_lock^2 | z_key^2), mode 1 = coldot. cnt (zeroed
+// ints, one per 64 columns; left zeroed): one launch, the last chunk's workgroup sums; else two.
 hipError_t launch_colstats(int mode, const float* z, int B, int L, int ldz, const float* colsq,
-                           const float* draw, float* part, int nchunk, float* out, hipStream_t st);
+                           const float* draw, float* part, int nchunk, float* out, hipStream_t st,
+                           int* cnt = nullptr);
 int colstats_nchunk(int B);
 hipError_t launch_metric(const float* z, int ldz, const float* rowfwd, const float* rowpart, int nblk,
                          const float* areas, const float* colsq, int B, int L, int metric, int recip,

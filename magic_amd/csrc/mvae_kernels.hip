@@ -461,9 +461,13 @@ __global__ void latent_fwd_kernel(const float* __restrict__ ms, EpsSrc es, float
 constexpr int CS_ROWS = 128;
 constexpr int CS_PER = CS_ROWS / 4;  // rows per thread
 
+// cnt (one launch): the partials written through (sc1) and counted per column block by an
+// agent-scope add after every storing wave's vmcnt(0); the block whose add comes last sums the
+// column block's partials in chunk order by sc1 loads -- colstats_final_kernel's order, so the
+// same bits -- and resets the counter (MI355X_MICROARCH.md's sc1 hand-off, first row)
 __global__ void colstats_part_kernel(int mode, const float* __restrict__ z, int B, int L, int ldz,
                                      const float* __restrict__ colsq, const float* __restrict__ draw,
-                                     float* __restrict__ part) {
+                                     float* __restrict__ part, int* __restrict__ cnt, float* __restrict__ out) {
   const int ncols = mode == 0 ? 2 * L : L;
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 cols x 4 row lanes
   const int j = blockIdx.x * 64 + tx;
@@ -499,8 +503,38 @@ __global__ void colstats_part_kernel(int mode, const float* __restrict__ z, int 
   }
   red[ty][tx] = acc;
   __syncthreads();
-  if (ty == 0 && j < ncols)
-    part[(size_t)blockIdx.y * ncols + j] = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
+  const float v = ((red[0][tx] + red[1][tx]) + red[2][tx]) + red[3][tx];
+  if (!cnt) {
+    if (ty == 0 && j < ncols) part[(size_t)blockIdx.y * ncols + j] = v;
+    return;
+  }
+  if (ty == 0 && j < ncols) __hip_atomic_store(part + (size_t)blockIdx.y * ncols + j, v, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  __shared__ int last;
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(cnt + blockIdx.x, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+           (int)gridDim.y - 1;
+  __syncthreads();
+  if (!last) return;
+  if (ty == 0 && j < ncols) {
+    const int nchunk = gridDim.y;
+    float a = 0.f;
+    int c = 0;
+    for (; c + 8 <= nchunk; c += 8) {  // (colstats_final_kernel's order)
+      float t[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        t[i] = __hip_atomic_load(part + (size_t)(c + i) * ncols + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) a += t[i];
+    }
+    for (; c < nchunk; ++c)
+      a += __hip_atomic_load(part + (size_t)c * ncols + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    out[j] = a;
+  }
+  if (threadIdx.x == 0) cnt[blockIdx.x] = 0;  // (the next launch is ordered behind this one)
 }
 
 __global__ void colstats_final_kernel(const float* __restrict__ part, int nchunk, int ncols,
@@ -1101,11 +1135,12 @@ hipError_t launch_latent_fwd(const float* ms, const LatentEps& le, float* z, con
 int colstats_nchunk(int B) { return (B + CS_ROWS - 1) / CS_ROWS; }
 
 hipError_t launch_colstats(int mode, const float* z, int B, int L, int ldz, const float* colsq,
-                           const float* draw, float* part, int nchunk, float* out, hipStream_t st) {
+                           const float* draw, float* part, int nchunk, float* out, hipStream_t st, int* cnt) {
   const int ncols = mode == 0 ? 2 * L : L;
   dim3 g(nblocks(ncols, 64), nchunk);
-  hipLaunchKernelGGL(colstats_part_kernel, g, dim3(256), 0, st, mode, z, B, L, ldz, colsq, draw, part);
-  hipLaunchKernelGGL(colstats_final_kernel, dim3(nblocks(ncols, 256)), dim3(256), 0, st, part, nchunk, ncols, out);
+  hipLaunchKernelGGL(colstats_part_kernel, g, dim3(256), 0, st, mode, z, B, L, ldz, colsq, draw, part, cnt, out);
+  if (!cnt)
+    hipLaunchKernelGGL(colstats_final_kernel, dim3(nblocks(ncols, 256)), dim3(256), 0, st, part, nchunk, ncols, out);
   return hipGetLastError();
 }
 

@@ -187,11 +187,19 @@ def test_xbw_split_steps_bitwise(case):
         cfg = preset("8c", image_size=20, batch=320, precision="bf16").replace(enc=(300, 260, 280))
     else:
         cfg = baseline_config(case)
+    _steps_bitwise(cfg, "xbw_split=0", "xbw_split=1")
+
+
+def _steps_bitwise(cfg, opt_a, opt_b):
+    """Three training steps (the second batch grey) under two create options: bitwise identical
+    parameters and losses."""
+    from magic_amd.engine import Engine
+    from tests.gpu_helpers import make_params
     P = make_params(cfg)
     batches = _batches(cfg, 3, 1, 11)
     res = []
-    for split in (0, 1):
-        eng = Engine(cfg.replace(options=f"xbw_split={split}"), 0)
+    for opt in (opt_a, opt_b):
+        eng = Engine(cfg.replace(options=opt), 0)
         try:
             eng.load_params(P)
             L = []
@@ -206,3 +214,20 @@ def test_xbw_split_steps_bitwise(case):
     assert torch.equal(l0, l1), (l0, l1)
     for k in p0:
         assert torch.equal(p0[k], p1[k]), k
+
+
+# ------------------------------------------------------------------ one-launch column statistics
+
+@pytest.mark.parametrize("case", ["C2", "C3", "wide"])
+def test_cs_one_steps_bitwise(case):
+    """Option cs_one: the cosine metric's column statistics (colsq, coldot; 8c/vae.py:449-450) in
+    one launch whose last chunk's workgroup sums the partials in the two-launch form's order -- the
+    same bits over three steps, at C2 (64 row chunks, one column block) and at a ragged shape with
+    several column blocks (L = 100: 200 colsq columns; B = 1000: a partial last chunk)."""
+    from magic_amd.config import baseline_config, preset
+    if case == "wide":
+        cfg = preset("8c", image_size=20, batch=1000, precision="bf16").replace(latent=100)
+    else:
+        cfg = baseline_config(case)
+    assert cfg.metric == "cosine"
+    _steps_bitwise(cfg, "cs_one=0", "cs_one=1")
