@@ -518,22 +518,30 @@ __global__ void colstats_part_kernel(int mode, const float* __restrict__ z, int 
            (int)gridDim.y - 1;
   __syncthreads();
   if (!last) return;
-  if (ty == 0 && j < ncols) {
-    const int nchunk = gridDim.y;
-    float a = 0.f;
-    int c = 0;
-    for (; c + 8 <= nchunk; c += 8) {  // (colstats_final_kernel's order)
-      float t[8];
+  // every row lane loads a quarter of each 64-chunk group (one round of load latency), row lane 0
+  // sums the column in chunk order (colstats_final_kernel's order: the same bits)
+  __shared__ float stage[64][64];
+  const int nchunk = gridDim.y;
+  float a = 0.f;
+  for (int c0 = 0; c0 < nchunk; c0 += 64) {
+    const int n = min(64, nchunk - c0);
+    if (j < ncols) {
+      float t[16];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        t[i] = __hip_atomic_load(part + (size_t)(c + i) * ncols + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int i = 0; i < 16; ++i) {
+        const int c = ty + 4 * i;
+        t[i] = c < n ? __hip_atomic_load(part + (size_t)(c0 + c) * ncols + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                     : 0.f;
+      }
 #pragma unroll
-      for (int i = 0; i < 8; ++i) a += t[i];
+      for (int i = 0; i < 16; ++i) stage[ty + 4 * i][tx] = t[i];
     }
-    for (; c < nchunk; ++c)
-      a += __hip_atomic_load(part + (size_t)c * ncols + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    out[j] = a;
+    __syncthreads();
+    if (ty == 0 && j < ncols)
+      for (int c = 0; c < n; ++c) a += stage[c][tx];
+    __syncthreads();
   }
+  if (ty == 0 && j < ncols) out[j] = a;
   if (threadIdx.x == 0) cnt[blockIdx.x] = 0;  // (the next launch is ordered behind this one)
 }
 
