@@ -218,7 +218,9 @@ typedef __attribute__((address_space(3))) short lds_short;
 // per thread (NW waves x 64 lanes x 16 B each)
 template <bool KC, int BK, int ROWS = 256, int NW = 8>
 struct WLoad {
-  static constexpr int NG = ROWS * BK / (NW * 512);
+  // (an image of 192 rows x 32 k is 1.5 instructions per thread: the last one by half the waves)
+  static constexpr int NCH = ROWS * BK / 8;  // 16-B chunks per image
+  static constexpr int NG = (NCH + NW * 64 - 1) / (NW * 64);
   static constexpr int CPR = BK / 8;    // 16-B chunks per row of a k-contiguous image
   static constexpr int RPB = 128 / BK;  // k-contiguous rows per 256-B bank row
   static constexpr int CPK = ROWS / 8;  // 16-B chunks per k-row of a row-contiguous image
@@ -252,6 +254,8 @@ struct WLoad {
                                         int kend, short* img, int wave) const {
 #pragma unroll
     for (int j = 0; j < NG; ++j) {
+      if constexpr (NCH % (NW * 64) != 0)
+        if ((j * NW + wave) * 64 >= NCH) continue;  // (wave-uniform)
       const bool ok = rv[j] && k0 + kc[j] < kend;
       const unsigned short* src = KC ? g + off[j] + k0 : g + off[j] + (long long)k0 * ld;
       src = ok ? src : reinterpret_cast<const unsigned short*>(g_zero16);
@@ -591,6 +595,184 @@ hipError_t launch_q_t(const PParams& p, bool at, bool bt, hipStream_t st) {
   return p.g.tn == 128 ? launch_q_l<EPI, TE, 128>(p, at, bt, st) : launch_q_l<EPI, TE, 256>(p, at, bt, st);
 }
 
+// ---------------------------------------------------------------------------------------
+// Plane-stacked f32x ring kernel (create option x3; tile TM x 128, TM = 64 MI). The ring kernel
+// above walks (k-tile, plane pair) iterations: six pairs make six iterations per 64 k, each with its
+// own barrier and image copies (3 A + 5 B images per k-tile) and two fragment reads per MFMA. Here
+// one stage holds a 32-k tile of EVERY plane the pairs read (A planes 0..NA-1, B planes 0..NB-1; two
+// stages, 120 / 144 KB), each k16-step reads every plane's fragments once and issues all its pair
+// MFMAs from them: per 64 k two barriers, 3 + 3 images and one fragment read per MFMA for each
+// pair -- the short-K f32x GEMMs of the hidden layers (K = 501: 48 ring iterations per tile) are
+// bound by those per-iteration costs, not by their MFMAs. The same pairs as the ring kernel
+// (i + j < 3, sum of 2^-24-exact plane products), summed (k16-step, pair) instead of (pair, k16).
+// The epilogues are the ring kernel's (32x32 accumulators, TN = 128: one per 32 rows per wave).
+constexpr __host__ __device__ int x3_pa(int na, int nb, int i) {
+  return na == 1 ? 0 : (nb == 1 ? i : (i < 3 ? 0 : (i == 5 ? 2 : 1)));  // (0,0) (0,1) (0,2) (1,1) (1,0) (2,0)
+}
+constexpr __host__ __device__ int x3_pb(int na, int nb, int i) {
+  return nb == 1 ? 0 : (na == 1 ? i : (i < 3 ? i : (i == 3 ? 1 : 0)));
+}
+template <int NA, int NB, int MI, bool AT, bool BT>
+__device__ __forceinline__ void x3_kloop(const PParams& pp, const Tile& t, const unsigned short* __restrict__ A,
+                                         const unsigned short* __restrict__ Bm, short* smem,
+                                         f32x16 (&acc)[MI][1], int wave, int lane, int wm, int wn) {
+  constexpr int BK = 32, TM = 64 * MI, TN = 128;
+  constexpr int IMA = TM * BK, IMB = TN * BK, STG = 3 * IMA + 3 * IMB;
+  constexpr int NP = (NA == 1 || NB == 1) ? 3 : 6;  // pairs i + j < 3
+  constexpr int NF = NB + NA * MI;                   // fragments per k16-step (B first)
+  constexpr int NM = NP * MI;                        // MFMAs per wave per k16-step
+  constexpr int H = NM / 2;                          // MFMAs before the stage hand-off
+  const Params& p = pp.g;
+  WLoad<!AT, BK, TM> la;
+  WLoad<BT, BK, TN> lb;
+  la.init(p.lda, t.m0, p.M, wave, lane);
+  lb.init(p.ldb, t.n0, p.N, wave, lane);
+  const int nkt = t.ks < t.ke ? (t.ke - t.ks + BK - 1) / BK : 0;
+  const bool sprio = (pp.diag & 32) == 0;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
+  auto issue = [&](int kt, int st) {
+    const int k0 = t.ks + kt * BK;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) la.issue(A + a * pp.pA, p.lda, k0, t.ke, smem + st * STG + a * IMA, wave);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) lb.issue(Bm + b * pp.pB, p.ldb, k0, t.ke, smem + st * STG + 3 * IMA + b * IMB, wave);
+  };
+  bf16x8 fa[2][NA][MI], fb[2][NB];
+  // fragment f of k16-step ks of stage st into buffer buf: the B planes' first, then A's by plane
+  auto rd_f = [&](int st, int ks, int f, int buf) {
+    if (f < NB) {
+      const int o = st * STG + 3 * IMA + f * IMB;
+      fb[buf][f] = lb.frag(smem + o, lds0 + 2u * (unsigned)o, wn * 32, ks, lane);
+    } else {
+      const int a = (f - NB) / MI, mi = (f - NB) % MI;
+      const int o = st * STG + a * IMA;
+      fa[buf][a][mi] = la.frag(smem + o, lds0 + 2u * (unsigned)o, wm * (MI * 32) + mi * 32, ks, lane);
+    }
+  };
+  auto mfma = [&](int i, int cur) {
+    const int pr = i / MI, mi = i % MI;
+    acc[mi][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][x3_pa(NA, NB, pr)][mi], fb[cur][x3_pb(NA, NB, pr)],
+                                                         acc[mi][0], 0, 0, 0);
+  };
+  if (nkt <= 0) return;
+  // prologue: stages 0 and 1 in flight, wait for both (one wait: waves issue unequal counts of
+  // a 192-row image), step 0's fragments
+  issue(0, 0);
+  if (nkt > 1) issue(1, 1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+#pragma unroll
+  for (int f = 0; f < NF; ++f) rd_f(0, 0, f, 0);
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int st = kt & 1;
+    // k16-step 0: its fragments landed; step 1's read into buffer 1 between the MFMAs
+    wait_lds<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    if (sprio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < NM; ++i) {
+      mfma(i, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int f = 0; f < NF; ++f)
+        if (f * NM / NF == i) rd_f(st, 1, f, 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (sprio) __builtin_amdgcn_s_setprio(0);
+    // k16-step 1: once its fragments are in registers this wave reads stage st no more; after
+    // half its MFMAs wait for stage st ^ 1 (k-tile kt + 1, the only copy in flight), one barrier
+    // (every wave done with stage st), then the copy of k-tile kt + 2 into stage st and the next
+    // k-tile's step-0 fragments behind the remaining MFMAs
+    wait_lds<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    if (sprio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < H; ++i) mfma(i, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    const bool more = kt + 1 < nkt;
+    if (more) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = H; i < NM; ++i) {
+      mfma(i, 1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (more) {
+#pragma unroll
+        for (int f = 0; f < NF; ++f)
+          if (f * (NM - H - 1) / NF + H == i) rd_f(st ^ 1, 0, f, 0);
+        if (i == NM - 2 && kt + 2 < nkt) issue(kt + 2, st);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (sprio) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <bool AT, bool BT, int EPI, bool TE, int MI>
+__global__ __launch_bounds__(WNT, 1) void gemm_bf16x_kernel(PParams pp) {
+  constexpr int TM = 64 * MI, TN = 128;
+  static_assert(MI == 4 || (MI == 3 && !AT), "192-row tiles need a k-contiguous A operand");
+  const Params& p = pp.g;
+  if (epi_skip<EPI>(p.epi)) return;
+  constexpr int RING = 2 * (3 * TM * 32 + 3 * TN * 32);
+  constexpr int EPIL = TE ? 2 * (2 * 64 * TN + 64 * MI * (TN / 8)) : 0;
+  __shared__ __attribute__((aligned(16))) short smem[RING > EPIL ? RING : EPIL];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const Tile t = tile_of_t<TM, TN>(p, true);
+  const unsigned short* __restrict__ A = pp.A + t.bi * p.sA;
+  const unsigned short* __restrict__ Bm = pp.B + t.bi * p.sB;
+  f32x16 acc[MI][1];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][0][r] = 0.f;
+  if (!(pp.diag & 16)) {  // diag bit 4: the epilogue alone
+    if (pp.dyn && *pp.dyn == 0) x3_kloop<1, 3, MI, AT, BT>(pp, t, A, Bm, smem, acc, wave, lane, wm, wn);
+    else x3_kloop<3, 3, MI, AT, BT>(pp, t, A, Bm, smem, acc, wave, lane, wm, wn);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (TE) epilogue_rm<EPI, MI, 1, 4, WNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag, nullptr,
+                                                    reinterpret_cast<float*>(smem) + 2 * 64 * TN);
+  else epilogue_g<EPI, MI, 1, TM, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
+}
+
+template <int EPI, bool TE>
+hipError_t launch_x_t(const PParams& p, bool at, bool bt, hipStream_t st) {
+  const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
+  const dim3 g(nwg), b(WNT);
+  if (p.g.tm == 192 && !at) {
+    if (bt) hipLaunchKernelGGL((gemm_bf16x_kernel<false, true, EPI, TE, 3>), g, b, 0, st, p);
+    else hipLaunchKernelGGL((gemm_bf16x_kernel<false, false, EPI, TE, 3>), g, b, 0, st, p);
+  } else if (!at && !bt) {
+    hipLaunchKernelGGL((gemm_bf16x_kernel<false, false, EPI, TE, 4>), g, b, 0, st, p);
+  } else if (at && !bt) {
+    hipLaunchKernelGGL((gemm_bf16x_kernel<true, false, EPI, TE, 4>), g, b, 0, st, p);
+  } else if (!at && bt) {
+    hipLaunchKernelGGL((gemm_bf16x_kernel<false, true, EPI, TE, 4>), g, b, 0, st, p);
+  } else {
+    hipLaunchKernelGGL((gemm_bf16x_kernel<true, true, EPI, TE, 4>), g, b, 0, st, p);
+  }
+  return hipGetLastError();
+}
+
+// the plane-stacked kernel serves this ring plan: option x3, tile N 128, the six f32x pairs of
+// three-plane operands (A's residual planes possibly zero at run time: its three-pair loop)
+bool x3_serves(const PParams& p) {
+  if (!p.x3 || p.g.tn != 128 || p.npairs != 6) return false;
+  for (int i = 0; i < 6; ++i)
+    if (p.pa[i] != x3_pa(3, 3, i) || p.pb[i] != x3_pb(3, 3, i)) return false;
+  return !p.dyn || p.npairs0 == 3;
+}
+
 // the row-major 16-B epilogue (epilogue_wide) applies: bases and strides keep every 8-column
 // chunk of every operand it touches 16-B aligned
 bool wide_epi_vec_ok(const Params& g) {
@@ -622,8 +804,9 @@ hipError_t launch_wide(const PParams& p, bool at, bool bt, int variant, hipStrea
     (void)variant;
     return gemm_bf16e_launch(p, at, bt, EPI, wide_epi_vec_ok(p.g), st);
   }
-  if ((p.g.epi.cp || BCE) && variant != 10 && wide_epi_vec_ok(p.g))
-    return launch_q_t<EPI, true>(p, at, bt, st);
+  const bool te = (p.g.epi.cp || BCE) && variant != 10 && wide_epi_vec_ok(p.g);
+  if (x3_serves(p)) return te ? launch_x_t<EPI, true>(p, at, bt, st) : launch_x_t<EPI, false>(p, at, bt, st);
+  if (te) return launch_q_t<EPI, true>(p, at, bt, st);
   return launch_q_t<EPI, false>(p, at, bt, st);
 }
 
@@ -774,6 +957,7 @@ hipError_t gemm_bf16_launch(const gemm::Params& g, const GemmDesc& d, int epi, h
   p.dj = d.dj;
   p.bits_reg = d.bits_reg;
   p.prio = d.prio;
+  p.x3 = d.x3;
   // the fused de-interleave rides on the eight-phase kernel's bits path only
   if (d.dj.nworkers && (g.tn != TN_E8 || !d.Abits || d.at || d.bt || (epi != EPI_STORE && epi != EPI_ACT)))
     return hipErrorInvalidValue;

@@ -54,6 +54,7 @@ struct PParams {
   DeintJob dj;                      // eight-phase kernel: the fused de-interleave (GemmDesc::dj)
   int bits_reg = 0;                 // eight-phase bits path: A words by loads to registers (E8 BITS 2)
   int prio = 0;                     // eight-phase kernel: s_setprio form (gemm_bf16e.hip e8_tile)
+  int x3 = 0;                       // f32x ring plans at tile N 128: the plane-stacked kernel (GemmDesc::x3)
 };
 
 // tanh as an odd [13/6] rational in x on [-7.905, 7.905] (clamped beyond, where tanh rounds to

@@ -475,6 +475,7 @@ struct CreateOpts {
   int adam_nt = 1;      // Adam's moment / fp32 parameter stores non-temporal (C2 -0.6 %, C3 -0.3 %, r6za)
   int deint_variant = 0;  // the bits de-interleave's form (launch_deint_bits; diagnostics / A-B)
   int e8_prio = 0;      // the eight-phase kernel's s_setprio form (PParams::prio; A-B)
+  int x3 = 0;           // f32x: ring plans at tile N 128 on the plane-stacked kernel (gemm_bf16.hip)
   int cs_one = 1;       // the column statistics in one launch (the last chunk's workgroup sums the
                         // partials in colstats_final_kernel's order: the same bits)
   int xbw_split = 2;    // the weight gradient's BitMat transposed from the forward's (mvae_ctx):
@@ -521,6 +522,7 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "e8_prio" && in(0, 2)) o->e8_prio = (int)v;
     else if (k == "xbw_split" && in(0, 2)) o->xbw_split = (int)v;
     else if (k == "cs_one" && in(0, 1)) o->cs_one = (int)v;
+    else if (k == "x3" && in(0, 1)) o->x3 = (int)v;
     else if (k == "enc_chain_rows" && (v == 0 || (in(16, 96) && v % 16 == 0))) o->enc_chain_rows = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
     else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
@@ -752,6 +754,7 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
   }
   auto wire = [&](GemmDesc& d) {
     d.prec = gp;
+    d.x3 = opt.x3;
     // skinny products (an output dimension or K <= 64 and no 256x256 plane-kernel shape: the
     // latent head and the decoder's first layer at small L) run on the fp32 VALU kernel
     const long long t256 = (long long)((d.M + 255) / 256) * ((d.N + 255) / 256) * d.batch;
@@ -1925,6 +1928,7 @@ extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int
   d.variant = (epi >> 8) & 15;
   if (d.variant == 9) { d.valu = 1; d.prec = GEMM_F32; d.variant = 0; }  // the fp32 VALU kernel
   if ((epi >> 13) & 1) d.tm = 192;  // epi bit 13: the ring kernel's 192-row tiles where eligible
+  d.x3 = (epi >> 16) & 1;           // epi bit 16: f32x ring plans at tile N 128 on the plane-stacked kernel
   d.epi.act = act;
   d.epi.aux = aux;
   d.epi.ld_aux = ld_aux;

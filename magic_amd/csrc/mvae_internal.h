@@ -135,6 +135,7 @@ struct GemmDesc {
   const int* anb = nullptr;
   DeintJob dj;                         // the fused de-interleave (eight-phase bits path only)
   int bits_reg = 0;                    // bits path: A words by loads to registers (gemm_bf16e.hip E8)
+  int x3 = 0;                          // f32x ring plans at tile N 128 on the plane-stacked kernel (gemm_bf16.hip)
   int prio = 0;                        // eight-phase kernel: s_setprio form (PParams::prio)
   GemmEpi epi;
 };
