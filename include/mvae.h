@@ -140,8 +140,10 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out);
  * the de-interleave; 2 = where the layer-0 forward leaves CUs idle, default), adam_nt (0/1: Adam's
  * moments and fp32 parameters stored non-temporal, default 1), e8_prio (0-2, A/B: the eight-phase
  * kernel's s_setprio form, default 0), deint_variant (0-6, A/B: the de-interleave's form), cs_one
- * (0/1: the cosine metric's column statistics in one launch, the last row chunk's workgroup
- * summing the partials in the two-launch order -- the same bits; default 1). Diagnostics, results
+ * (0-2: the cosine metric's column statistics in one launch, the last row chunk's workgroup
+ * summing the partials in the two-launch order -- the same bits; 2, the default: where L <= 32),
+ * x3 (0/1: f32x ring-kernel plans at tile N 128 on the plane-stacked kernel, every operand plane
+ * of a 32-k tile in LDS at once; the same products summed in another order). Diagnostics, results
  * meaningless: deint_fuse_diag (0-31: parts of the fused launch switched off), diag_skip_deint (1: de-interleave only the first batch -- a timing bound),
  * diag_shadow_deint (-1 or a workgroup count > 0: a second de-interleave of each step's input
  * into a scratch image on a low-priority stream, launched at diag_shadow_at = 0 the forward,

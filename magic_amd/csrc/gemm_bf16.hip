@@ -869,6 +869,7 @@ struct WidePlan { int split = 1; int tn = 256; int tm = 256; };
 static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
   const bool fixed = d.epi.mode == EPI_BCE || d.epi.mode == EPI_BCEB || d.epi.mode == EPI_SIGMOID;
   const int kt = (d.K + 63) / 64;
+  const bool x3 = d.x3 && d.prec == GEMM_F32X && d.nA == 3 && d.nB == 3;
   const int T = d.nA > d.nB ? d.nA : d.nB;
   int np = 0;
   for (int i = 0; i < d.nA; ++i)
@@ -917,7 +918,10 @@ static WidePlan wide_plan(const GemmDesc& d, size_t max_ws) {
     // 256x128 tile does half the MFMA work per k-tile in ~1.5 us (profiles/r2/gemm_ab_tile_n.txt);
     // 192-row tiles interpolated (a fixed ~1.1 us per k-tile plus ~0.1 us per 32x32 block).
     // eight-phase kernel: per 256x256 k-tile (gemm_bf16e.hip)
-    const double t_kt = e8 ? 1.35e-6 : tmr == 192 ? (w == 256 ? 1.7e-6 : 1.4e-6) : (w == 256 ? 1.9e-6 : 1.5e-6);
+    double t_kt = e8 ? 1.35e-6 : tmr == 192 ? (w == 256 ? 1.7e-6 : 1.4e-6) : (w == 256 ? 1.9e-6 : 1.5e-6);
+    // the plane-stacked kernel (option x3) serves the six-pair f32x ring plans at tile N 128:
+    // C2 hidden forward 60 -> 50 us, hidden dgrad 72 -> 67 us in the region pass (r6zi)
+    if (x3 && !e8 && w == 128) t_kt *= 0.88;
     const double fix = 3.0;
     for (int s = 1; s <= (fixed ? 1 : 32); ++s) {
       if (s > 1 && kt / s < 2) break;

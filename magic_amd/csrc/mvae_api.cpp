@@ -476,8 +476,9 @@ struct CreateOpts {
   int deint_variant = 0;  // the bits de-interleave's form (launch_deint_bits; diagnostics / A-B)
   int e8_prio = 0;      // the eight-phase kernel's s_setprio form (PParams::prio; A-B)
   int x3 = 0;           // f32x: ring plans at tile N 128 on the plane-stacked kernel (gemm_bf16.hip)
-  int cs_one = 1;       // the column statistics in one launch (the last chunk's workgroup sums the
-                        // partials in colstats_final_kernel's order: the same bits)
+  int cs_one = 2;       // the column statistics in one launch (the last chunk's workgroup sums the
+                        // partials in colstats_final_kernel's order: the same bits): 0 off, 1 on, 2
+                        // where L <= 32 (one 64-column block: C2 -0.9 %; C3, L 200: +0.2 %, r6zh / r6zi)
   int xbw_split = 2;    // the weight gradient's BitMat transposed from the forward's (mvae_ctx):
                         // 0 off, 1 on, 2 where the layer-0 forward's workgroups leave >= 32 CUs
                         // (C3 -0.6 %, C5 -0.4 %; C2, 480 forward workgroups: +3.8 % on, r6zf)
@@ -521,7 +522,7 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "deint_variant" && in(0, 6)) o->deint_variant = (int)v;
     else if (k == "e8_prio" && in(0, 2)) o->e8_prio = (int)v;
     else if (k == "xbw_split" && in(0, 2)) o->xbw_split = (int)v;
-    else if (k == "cs_one" && in(0, 1)) o->cs_one = (int)v;
+    else if (k == "cs_one" && in(0, 2)) o->cs_one = (int)v;
     else if (k == "x3" && in(0, 1)) o->x3 = (int)v;
     else if (k == "enc_chain_rows" && (v == 0 || (in(16, 96) && v % 16 == 0))) o->enc_chain_rows = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
@@ -646,7 +647,7 @@ int mvae_create_ex(const mvae_cfg* cfg, int device, const char* options, mvae_ct
   ALLOC(c->colsq, 2 * L);
   ALLOC(c->coldot, L);
   ALLOC(c->cspart, (size_t)c->nchunk * 2 * L);
-  if (opt.cs_one) ALLOC(*reinterpret_cast<float**>(&c->cscnt), (2 * L + 63) / 64);  // (zeroed)
+  if (opt.cs_one == 1 || (opt.cs_one == 2 && L <= 32)) ALLOC(*reinterpret_cast<float**>(&c->cscnt), (2 * L + 63) / 64);  // (zeroed)
   ALLOC(c->eps, 3 * B * L);
   ALLOC(c->rowfwd, 4 * B);
   ALLOC(c->dzd2, B * c->ld_d2);

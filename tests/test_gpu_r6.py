@@ -230,4 +230,4 @@ def test_cs_one_steps_bitwise(case):
     else:
         cfg = baseline_config(case)
     assert cfg.metric == "cosine"
-    _steps_bitwise(cfg, "cs_one=0", "cs_one=1")
+    _steps_bitwise(cfg, "cs_one=0", "cs_one=1")  # (forced on: the default is on only where L <= 32)

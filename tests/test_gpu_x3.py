@@ -67,8 +67,11 @@ def test_x3_c2_step_vs_oracle():
 
 
 def test_x3_c2_steps_match_ring_kernel():
-    """Three C2 steps (the second batch grey) with and without x3: the same losses and parameters to
-    fp32 rounding (the same products in another summation order)."""
+    """C2 with and without x3 on the same inputs: both gradients of one backward to fp32 rounding
+    (the same plane products summed in another order), and the losses of three training steps (the
+    second batch grey). Parameters are not compared bitwise-close: TF-Adam's m / sqrt(v) turns a
+    rounding-level difference of a near-zero gradient into up to a learning-rate-sized step."""
+    from magic_amd import _lib as L_
     from magic_amd.config import baseline_config
     from magic_amd.engine import Engine
     from tests.gpu_helpers import make_params
@@ -81,16 +84,24 @@ def test_x3_c2_steps_match_ring_kernel():
         eng = Engine(cfg.replace(options=opt), 0)
         try:
             eng.load_params(P)
+            x, a = batches[0]
+            eng.forward(x)
+            eng.metric(a)
+            eng.backward()
+            torch.cuda.synchronize()
+            grads = {(kind, k): v.cpu().double() for kind in (L_.KIND_GRAD1, L_.KIND_GRAD2)
+                     for k, v in eng.tensors(kind).items()}
+            eng.load_params(P)
             L = []
             for x, a in batches:
                 eng.train_step(x, a)
                 L.append(eng.losses.clone())
             torch.cuda.synchronize()
-            res.append(({k: v.cpu().double() for k, v in eng.params().items()}, torch.stack(L).cpu().double()))
+            res.append((grads, torch.stack(L).cpu().double()))
         finally:
             eng.close()
-    (p0, l0), (p1, l1) = res
+    (g0, l0), (g1, l1) = res
     assert ((l0 - l1).abs() <= 1e-5 * l0.abs() + 1e-6).all(), (l0, l1)
-    for k in p0:
-        d = (p0[k] - p1[k]).abs().max().item()
-        assert d <= 1e-6 * p0[k].abs().max().item() + 1e-9, (k, d)
+    for k in g0:
+        d = (g0[k] - g1[k]).abs().max().item()
+        assert d <= 2e-5 * g0[k].abs().max().item() + 1e-12, (k, d)
