@@ -1,11 +1,18 @@
 #!/bin/bash
-# The current GPU session (overwritten per session; earlier sessions are in git history):
-#   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r6zk: the final tree of round 6's second session (x3, cs_one) -- C2 / C3 timed-loop traces with
-# the dominant region marked, the default bench line (C2 headline + configs block, PMC passes)
+# r6zl: default-option re-check at C2 with x3 (same box, each against an adjacent default run)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-B="--no-cpu-baseline --pmc off --no-h2d --no-pipeline --no-configs --steps 20 --warmup 3 --mark-dominant"
-p() { echo "r6zk_prof_$1|240|cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/gpurun_out/prof_r6zk_$1 -o run -- python3 $PWD/bench.py --config $2 $B"; }
+A="--no-cpu-baseline --pmc off --no-h2d --no-pipeline --no-configs --steps 60 --warmup 5"
 bash tools/gpu_steps.sh \
-  "$(p c2 C2)" "$(p c3 C3)" \
-  "r6zk_bench|900|python bench.py > gpurun_out/r6zk_bench.json"
+  "r6zl_d1|200|python bench.py --config C2 $A" \
+  "r6zl_e80|200|python bench.py --config C2 $A --create-opt e8=0" \
+  "r6zl_d2|200|python bench.py --config C2 $A" \
+  "r6zl_bs0|200|python bench.py --config C2 $A --create-opt bce_split=0" \
+  "r6zl_d3|200|python bench.py --config C2 $A" \
+  "r6zl_tr1|200|python bench.py --config C2 $A --create-opt thin_ring=1" \
+  "r6zl_d4|200|python bench.py --config C2 $A" \
+  "r6zl_tr0|200|python bench.py --config C2 $A --create-opt thin_ring=0" \
+  "r6zl_d5|200|python bench.py --config C2 $A" \
+  "r6zl_ec2|200|python bench.py --config C2 $A --opt early_chunks=2" \
+  "r6zl_d6|200|python bench.py --config C2 $A" \
+  "r6zl_sm1|200|python bench.py --config C2 $A --opt side_mask=1" \
+  "r6zl_d7|200|python bench.py --config C2 $A"
