@@ -637,9 +637,13 @@ __device__ __forceinline__ void x3_kloop(const PParams& pp, const Tile& t, const
 #pragma unroll
     for (int b = 0; b < NB; ++b) lb.issue(Bm + b * pp.pB, p.ldb, k0, t.ke, smem + st * STG + 3 * IMA + b * IMB, wave);
   };
+  // a wave whose 32 columns all lie past N (the latent head's N = 2L = 40 in a 128-wide tile)
+  // issues no fragment reads and no MFMAs: its outputs are never stored (it still copies and syncs)
+  const bool live = t.n0 + wn * 32 < p.N;
   bf16x8 fa[2][NA][MI], fb[2][NB];
   // fragment f of k16-step ks of stage st into buffer buf: the B planes' first, then A's by plane
   auto rd_f = [&](int st, int ks, int f, int buf) {
+    if (!live) return;
     if (f < NB) {
       const int o = st * STG + 3 * IMA + f * IMB;
       fb[buf][f] = lb.frag(smem + o, lds0 + 2u * (unsigned)o, wn * 32, ks, lane);
@@ -651,8 +655,9 @@ __device__ __forceinline__ void x3_kloop(const PParams& pp, const Tile& t, const
   };
   auto mfma = [&](int i, int cur) {
     const int pr = i / MI, mi = i % MI;
-    acc[mi][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][x3_pa(NA, NB, pr)][mi], fb[cur][x3_pb(NA, NB, pr)],
-                                                         acc[mi][0], 0, 0, 0);
+    if (live)
+      acc[mi][0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][x3_pa(NA, NB, pr)][mi], fb[cur][x3_pb(NA, NB, pr)],
+                                                           acc[mi][0], 0, 0, 0);
   };
   if (nkt <= 0) return;
   // prologue: stages 0 and 1 in flight, wait for both (one wait: waves issue unequal counts of
