@@ -63,6 +63,36 @@ __device__ __forceinline__ void deint_load(const float4* __restrict__ x, int D, 
     }
   }
 }
+// The same registers loaded coalesced: pass i's 16 rows x 96 float4 (the task's 1.5 KB of each row)
+// read by consecutive lanes (one 1 KB contiguous span per wave instruction, where deint_load's
+// lanes stride 96 B: each instruction then touches 48 lines of 128 B), passed through an LDS stage
+// (two buffers of 24 KB, pass parity) into deint_load's mapping (row tid / 16 + 16 i, octet
+// tid % 16). PB 2, 256 threads only. Float4s past the row's end (pixels past D, unused) read its last.
+__device__ __forceinline__ void deint_load_co(const float4* __restrict__ x, int D, int bx, int by,
+                                              float4 (&v)[4][6], float4 (*stage)[16][96]) {
+  const int tid = threadIdx.x;
+  const int b0 = by * 64, c40 = 3 * (bx * 128) / 4, rowf4 = 3 * D / 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int q = tid + 256 * k, r = q / 96, c4 = min(c40 + q % 96, rowf4 - 1);
+      v[i][k] = x[(size_t)(b0 + 16 * i + r) * rowf4 + c4];
+    }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float4 (*st)[96] = stage[i & 1];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+      const int q = tid + 256 * k;
+      st[q / 96][q % 96] = v[i][k];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 6; ++k) v[i][k] = st[tid / 16][6 * (tid % 16) + k];
+  }
+}
+
 // one row's 8 pixels x 3 channels (interleaved, as X stores them) -> the byte of each block
 // (bit j = pixel j nonzero; block c: rot, lock, key <- channels 1, 0, 2); true if a value is not
 // 0 / 1
@@ -180,13 +210,19 @@ __device__ __forceinline__ void deint_finish(int B, int D, int kts_f, int kts_w,
 }
 
 // the whole task (the standalone kernel's workgroup)
-template <int PB, int NT, int OS, bool NTL = false, bool NOW = false>
+template <int PB, int NT, int OS, bool NTL = false, bool NOW = false, bool CO = false>
 __device__ __forceinline__ void deint_bits_task(const float4* __restrict__ x, int B, int D, int kts_f, int kts_w,
                                                 unsigned* __restrict__ xbf, unsigned* __restrict__ xbw,
                                                 unsigned char* __restrict__ xbits, int ldbits,
-                                                int* __restrict__ dyn, int bx, int by, DeintLds<PB, OS>& bt) {
+                                                int* __restrict__ dyn, int bx, int by, DeintLds<PB, OS>& bt,
+                                                float4 (*stage)[16][96] = nullptr) {
   float4 v[DeintShape<PB, NT>::NR][6];
-  deint_load<PB, NT, NTL>(x, D, bx, by, v);
+  if constexpr (CO) {
+    static_assert(PB == 2 && NT == 256, "the coalesced load serves the step's task shape");
+    deint_load_co(x, D, bx, by, v, stage);
+  } else {
+    deint_load<PB, NT, NTL>(x, D, bx, by, v);
+  }
   auto none = [] {};
   deint_finish<PB, NT, OS, false, decltype(none)&, decltype(none)&, NOW>(B, D, kts_f, kts_w, xbf, xbw, xbits,
                                                                          ldbits, dyn, bx, by, v, bt, none, none);

@@ -883,7 +883,7 @@ __global__ __launch_bounds__(256) void make_batch4_kernel(const unsigned char* _
 // The layer-0 pixel operand of a 0/1 batch as BitMats (deint_bits.h): one workgroup per task of
 // 64 batch rows x 64 PB pixels. Raises the not-binary word (*dyn slot 2) when a pixel is neither 0
 // nor 1: the step then runs deint_grey_kernel (the planes) and the GEMMs read the planes.
-template <int PB, int NT, int OS, bool NTL = false, bool NOW = false>
+template <int PB, int NT, int OS, bool NTL = false, bool NOW = false, bool CO = false>
 __global__ __launch_bounds__(NT) void deint_bits_kernel(const float4* __restrict__ x, int B, int D, int kts_f,
                                                         int kts_w, unsigned* __restrict__ xbf,
                                                         unsigned* __restrict__ xbw,
@@ -891,7 +891,14 @@ __global__ __launch_bounds__(NT) void deint_bits_kernel(const float4* __restrict
                                                         int* __restrict__ dyn, int* __restrict__ dyn_next) {
   if (dyn_next && (blockIdx.x | blockIdx.y | threadIdx.x) == 0) dyn_next[0] = dyn_next[2] = 0;
   __shared__ __attribute__((aligned(16))) DeintLds<PB, OS> bt;
-  deint_bits_task<PB, NT, OS, NTL, NOW>(x, B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, blockIdx.x, blockIdx.y, bt);
+  if constexpr (CO) {
+    __shared__ __attribute__((aligned(16))) float4 stage[2][16][96];
+    deint_bits_task<PB, NT, OS, NTL, NOW, true>(x, B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, blockIdx.x,
+                                                blockIdx.y, bt, stage);
+  } else {
+    deint_bits_task<PB, NT, OS, NTL, NOW>(x, B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, blockIdx.x, blockIdx.y,
+                                          bt);
+  }
 }
 
 // The weight gradient's BitMat (pixels x stacked rows) from the forward's (stacked rows x
@@ -1045,6 +1052,14 @@ hipError_t launch_deint_bits(const float* x, int B, int D, unsigned* xbf, int kt
     case 7:  // the step's form without the weight-gradient words (launch_bits_transpose writes them)
       hipLaunchKernelGGL((deint_bits_kernel<2, 256, 72, false, true>), dim3((kts_f + 1) / 2, B / 64), dim3(256), 0, st,
                          x4, B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
+      break;
+    case 8:  // the step's form with coalesced loads of X through an LDS stage (deint_load_co)
+      hipLaunchKernelGGL((deint_bits_kernel<2, 256, 72, false, false, true>), dim3((kts_f + 1) / 2, B / 64), dim3(256), 0,
+                         st, x4, B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
+      break;
+    case 9:  // variant 7 with coalesced loads
+      hipLaunchKernelGGL((deint_bits_kernel<2, 256, 72, false, true, true>), dim3((kts_f + 1) / 2, B / 64), dim3(256), 0,
+                         st, x4, B, D, kts_f, kts_w, xbf, xbw, xbits, ldbits, dyn, dyn_next);
       break;
     case 6:  // the step's form with non-temporal loads of X (2x slower: r6zb_deint_nt_loads.txt)
       hipLaunchKernelGGL((deint_bits_kernel<2, 256, 72, true>), dim3((kts_f + 1) / 2, B / 64), dim3(256), 0, st, x4, B,

@@ -231,3 +231,19 @@ def test_cs_one_steps_bitwise(case):
         cfg = baseline_config(case)
     assert cfg.metric == "cosine"
     _steps_bitwise(cfg, "cs_one=0", "cs_one=1")  # (forced on: the default is on only where L <= 32)
+
+
+# ------------------------------------------------------------------ coalesced de-interleave loads
+
+@pytest.mark.parametrize("case", ["C3", "C2", "small"])
+def test_deint_coalesced_steps_bitwise(case):
+    """deint_variant 8: the de-interleave's X loads coalesced through an LDS stage (deint_load_co)
+    -- the same BitMats, target bits and not-binary word, so three steps (the second batch grey)
+    are bitwise the default's; C3 takes its weight-gradient-words-free form (xbw_split), C2 the
+    whole form, and the small shape (D = 400) a partial last pixel task."""
+    from magic_amd.config import baseline_config, preset
+    if case == "small":
+        cfg = preset("8c", image_size=20, batch=320, precision="bf16").replace(enc=(300, 260, 280))
+    else:
+        cfg = baseline_config(case)
+    _steps_bitwise(cfg, "", "deint_variant=8")

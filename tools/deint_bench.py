@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """A/B the de-interleave forms (mvae_bench_deint) at a config's batch shape, interleaved rounds in
-one process: ms per launch and GB/s of the bytes each form must move.
+one process: ms per launch and GB/s of the bytes each form must move (variant + 1000: four X
+images read in turn, so the last-level cache holds none of the next launch's input).
 
   python tools/deint_bench.py [--config C3] [--variants 100,0,1,2,3,4] [--rounds 3]
 """
@@ -42,7 +43,8 @@ def main():
     read = B * 3 * D * 4
     for v in vs:
         m = statistics.median(res[v])
-        wr = 3 * B * D * 2 + B * D / 8 if v == 100 else 2 * 3 * B * (D + 64) / 8 + B * D / 8
+        vv = v % 1000  # (v + 1000: four X images in turn, none cached)
+        wr = 3 * B * D * 2 + B * D / 8 if vv == 100 else 2 * 3 * B * (D + 64) / 8 + B * D / 8
         print(f"{a.config} variant {v:3d}: {m * 1e3:8.1f} us  {(read + wr) / m / 1e6:7.0f} GB/s "
               f"(read {read / 1e6:.0f} MB, write {wr / 1e6:.0f} MB)")
 
