@@ -139,7 +139,7 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out);
  * weight gradient's BitMat transposed from the forward's on the side stream instead of written by
  * the de-interleave; 2 = where the layer-0 forward leaves CUs idle, default), adam_nt (0/1: Adam's
  * moments and fp32 parameters stored non-temporal, default 1), e8_prio (0-2, A/B: the eight-phase
- * kernel's s_setprio form, default 0), deint_variant (0-6, A/B: the de-interleave's form), cs_one
+ * kernel's s_setprio form, default 0), deint_variant (0-6 or 8, A/B: the de-interleave's form; 8 = coalesced X loads through LDS), cs_one
  * (0-2: the cosine metric's column statistics in one launch, the last row chunk's workgroup
  * summing the partials in the two-launch order -- the same bits; 2, the default: where L <= 32),
  * x3 (0/1: f32x ring-kernel plans at tile N 128 on the plane-stacked kernel, every operand plane
