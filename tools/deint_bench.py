@@ -43,7 +43,7 @@ def main():
     read = B * 3 * D * 4
     for v in vs:
         m = statistics.median(res[v])
-        vv = v % 1000  # (v + 1000: four X images in turn, none cached)
+        vv = v % 1000  # (v + 1000: four X images in turn, none cached; + 2000 / 4000: a GEMM / 1 GB memset before each)
         wr = 3 * B * D * 2 + B * D / 8 if vv == 100 else 2 * 3 * B * (D + 64) / 8 + B * D / 8
         print(f"{a.config} variant {v:3d}: {m * 1e3:8.1f} us  {(read + wr) / m / 1e6:7.0f} GB/s "
               f"(read {read / 1e6:.0f} MB, write {wr / 1e6:.0f} MB)")

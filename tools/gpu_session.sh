@@ -1,13 +1,6 @@
 #!/bin/bash
-# The current GPU session (overwritten per session; earlier sessions are in git history):
-#   tools/gpu_go.sh tools/gpu_session.sh [timeout-seconds]
-# r6zn: the final tree -- whole GPU suite, smoke, C2 / C3 timed-loop traces, the default bench line
+# r6zo: the de-interleave right after a 1 ms bf16 GEMM on random operands (+2000) or a 1 GB memset
+# (+4000), each launch timed alone, against back-to-back launches -- why the in-step pass is slower
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-T="python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider"
-B="--no-cpu-baseline --pmc off --no-h2d --no-pipeline --no-configs --steps 20 --warmup 3 --mark-dominant"
-p() { echo "r6zn_prof_$1|240|cd /tmp && TMPDIR=/tmp rocprofv3 --kernel-trace --stats --output-format csv -d $PWD/gpurun_out/prof_r6zn_$1 -o run -- python3 $PWD/bench.py --config $2 $B"; }
 bash tools/gpu_steps.sh \
-  "r6zn_tests|1100|$T -m gpu tests" \
-  "r6zn_smoke|240|python -c 'import __graft_entry__ as g; g.smoke()'" \
-  "$(p c2 C2)" "$(p c3 C3)" \
-  "r6zn_bench|900|python bench.py > gpurun_out/r6zn_bench.json"
+  "r6zo_db|400|python tools/deint_bench.py --config C3 --variants 7,2007,4007,1007,3007,5007 --rounds 3 --iters 10 && python tools/deint_bench.py --config C2 --variants 0,2000,4000 --rounds 3 --iters 10"
