@@ -719,6 +719,115 @@ __device__ __forceinline__ void x3_kloop(const PParams& pp, const Tile& t, const
   }
 }
 
+// The 256 x 256 form (the ring kernel's 256x256 plans: C2's hidden weight gradients): a 16-k stage
+// of all six planes is 48 KB, three stages; each k16-step reads its 18 fragments (A 3 x 4, B 3 x 2)
+// once, after the stage's barrier, and issues the 48 pair MFMAs from them -- no fragment double
+// buffer (18 + 128 accumulator registers; the other wave of the SIMD covers the read latency)
+template <int NA, int NB, bool AT, bool BT>
+__device__ __forceinline__ void x3w_kloop(const PParams& pp, const Tile& t, const unsigned short* __restrict__ A,
+                                          const unsigned short* __restrict__ Bm, short* smem,
+                                          f32x16 (&acc)[4][2], int wave, int lane, int wm, int wn) {
+  constexpr int BK = 16, TM = 256, TN = 256, MI = 4, NI = 2;
+  constexpr int IMA = TM * BK, IMB = TN * BK, STG = 3 * IMA + 3 * IMB;
+  constexpr int NP = (NA == 1 || NB == 1) ? 3 : 6;
+  constexpr int NG = NA * WLoad<!AT, BK, TM>::NG + NB * WLoad<BT, BK, TN>::NG;  // DMA instructions per stage
+  const Params& p = pp.g;
+  WLoad<!AT, BK, TM> la;
+  WLoad<BT, BK, TN> lb;
+  la.init(p.lda, t.m0, p.M, wave, lane);
+  lb.init(p.ldb, t.n0, p.N, wave, lane);
+  const int nkt = t.ks < t.ke ? (t.ke - t.ks + BK - 1) / BK : 0;
+  const bool sprio = (pp.diag & 32) == 0;
+  const unsigned lds0 = (unsigned)(uintptr_t)(lds_short*)smem;
+  const bool live = t.n0 + wn * (TN / 4) < p.N;
+  auto issue = [&](int kt, int st) {
+    const int k0 = t.ks + kt * BK;
+#pragma unroll
+    for (int a = 0; a < NA; ++a) la.issue(A + a * pp.pA, p.lda, k0, t.ke, smem + st * STG + a * IMA, wave);
+#pragma unroll
+    for (int b = 0; b < NB; ++b) lb.issue(Bm + b * pp.pB, p.ldb, k0, t.ke, smem + st * STG + 3 * IMA + b * IMB, wave);
+  };
+  if (nkt <= 0) return;
+  issue(0, 0);
+  if (nkt > 1) issue(1, 1);
+  for (int kt = 0; kt < nkt; ++kt) {
+    const int st = kt % 3;
+    // stage kt landed (only k-tile kt + 1's copies may still be in flight), every wave done with
+    // k-tile kt - 1's stage: the copy of kt + 2 goes into it
+    if (kt + 1 < nkt) {
+      if constexpr (NG == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if constexpr (NG == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + 2 < nkt) issue(kt + 2, (kt + 2) % 3);
+    if (!live) continue;
+    bf16x8 fa[NA][MI], fb[NB][NI];
+#pragma unroll
+    for (int b = 0; b < NB; ++b)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int o = st * STG + 3 * IMA + b * IMB;
+        fb[b][ni] = lb.frag(smem + o, lds0 + 2u * (unsigned)o, wn * (TN / 4) + ni * 32, 0, lane);
+      }
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) {
+        const int o = st * STG + a * IMA;
+        fa[a][mi] = la.frag(smem + o, lds0 + 2u * (unsigned)o, wm * (MI * 32) + mi * 32, 0, lane);
+      }
+    wait_lds<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    if (sprio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int pr = 0; pr < NP; ++pr)
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          acc[mi][ni] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[x3_pa(NA, NB, pr)][mi], fb[x3_pb(NA, NB, pr)][ni],
+                                                                acc[mi][ni], 0, 0, 0);
+    if (sprio) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <bool AT, bool BT, int EPI, bool TE>
+__global__ __launch_bounds__(WNT, 1) void gemm_bf16xw_kernel(PParams pp) {
+  constexpr int TM = 256, TN = 256;
+  const Params& p = pp.g;
+  if (epi_skip<EPI>(p.epi)) return;
+  constexpr int RING = 3 * (3 * TM * 16 + 3 * TN * 16);
+  constexpr int EPIL = TE ? 2 * (2 * 64 * TN + 64 * 4 * (TN / 8)) : 0;
+  __shared__ __attribute__((aligned(16))) short smem[RING > EPIL ? RING : EPIL];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const Tile t = tile_of_t<TM, TN>(p, true);
+  const unsigned short* __restrict__ A = pp.A + t.bi * p.sA;
+  const unsigned short* __restrict__ Bm = pp.B + t.bi * p.sB;
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  if (!(pp.diag & 16)) {
+    if (pp.dyn && *pp.dyn == 0) x3w_kloop<1, 3, AT, BT>(pp, t, A, Bm, smem, acc, wave, lane, wm, wn);
+    else x3w_kloop<3, 3, AT, BT>(pp, t, A, Bm, smem, acc, wave, lane, wm, wn);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (TE) epilogue_rm<EPI, 4, 2, 4, WNT>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn, pp.diag, nullptr,
+                                                   reinterpret_cast<float*>(smem) + 2 * 64 * TN);
+  else epilogue_g<EPI, 4, 2, TM, 4>(p, t, acc, reinterpret_cast<float*>(smem), wm, wn);
+}
+
 template <bool AT, bool BT, int EPI, bool TE, int MI>
 __global__ __launch_bounds__(WNT, 1) void gemm_bf16x_kernel(PParams pp) {
   constexpr int TM = 64 * MI, TN = 128;
@@ -754,6 +863,13 @@ template <int EPI, bool TE>
 hipError_t launch_x_t(const PParams& p, bool at, bool bt, hipStream_t st) {
   const int nwg = p.g.ntm * p.g.ntn * p.g.batch * p.g.split;
   const dim3 g(nwg), b(WNT);
+  if (p.g.tn == 256) {  // (x3_serves: 256-row tiles)
+    if (!at && !bt) hipLaunchKernelGGL((gemm_bf16xw_kernel<false, false, EPI, TE>), g, b, 0, st, p);
+    else if (at && !bt) hipLaunchKernelGGL((gemm_bf16xw_kernel<true, false, EPI, TE>), g, b, 0, st, p);
+    else if (!at && bt) hipLaunchKernelGGL((gemm_bf16xw_kernel<false, true, EPI, TE>), g, b, 0, st, p);
+    else hipLaunchKernelGGL((gemm_bf16xw_kernel<true, true, EPI, TE>), g, b, 0, st, p);
+    return hipGetLastError();
+  }
   if (p.g.tm == 192 && !at) {
     if (bt) hipLaunchKernelGGL((gemm_bf16x_kernel<false, true, EPI, TE, 3>), g, b, 0, st, p);
     else hipLaunchKernelGGL((gemm_bf16x_kernel<false, false, EPI, TE, 3>), g, b, 0, st, p);
@@ -772,7 +888,10 @@ hipError_t launch_x_t(const PParams& p, bool at, bool bt, hipStream_t st) {
 // the plane-stacked kernel serves this ring plan: option x3, tile N 128, the six f32x pairs of
 // three-plane operands (A's residual planes possibly zero at run time: its three-pair loop)
 bool x3_serves(const PParams& p) {
-  if (!p.x3 || p.g.tn != 128 || p.npairs != 6) return false;
+  if (!p.x3 || p.npairs != 6) return false;
+  if (p.g.tn != 128 && !(p.g.tn == 256 && p.g.tm == 256 && p.x3 >= 2)) return false;
+  // (the 256x256 form's BCE instantiations spill: the head keeps the eight-phase / ring kernels)
+  if (p.g.tn == 256 && (p.g.epi.mode == EPI_BCE || p.g.epi.mode == EPI_BCEB)) return false;
   for (int i = 0; i < 6; ++i)
     if (p.pa[i] != x3_pa(3, 3, i) || p.pb[i] != x3_pb(3, 3, i)) return false;
   return !p.dyn || p.npairs0 == 3;

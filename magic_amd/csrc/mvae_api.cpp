@@ -524,7 +524,7 @@ static int parse_opts(const char* s, CreateOpts* o) {
     else if (k == "e8_prio" && in(0, 2)) o->e8_prio = (int)v;
     else if (k == "xbw_split" && in(0, 2)) o->xbw_split = (int)v;
     else if (k == "cs_one" && in(0, 2)) o->cs_one = (int)v;
-    else if (k == "x3" && in(0, 1)) o->x3 = (int)v;
+    else if (k == "x3" && in(0, 2)) o->x3 = (int)v;
     else if (k == "enc_chain_rows" && (v == 0 || (in(16, 96) && v % 16 == 0))) o->enc_chain_rows = (int)v;
     else if (k == "conv2_nw" && (v == 4 || v == 8 || v == 16)) o->conv2_nw = (int)v;
     else if (k == "conv2_tpb" && in(1, 2)) o->conv2_tpb = (int)v;
@@ -1930,7 +1930,7 @@ extern "C" int mvae_debug_gemm(int M, int N, int K, const float* A, int lda, int
   d.variant = (epi >> 8) & 15;
   if (d.variant == 9) { d.valu = 1; d.prec = GEMM_F32; d.variant = 0; }  // the fp32 VALU kernel
   if ((epi >> 13) & 1) d.tm = 192;  // epi bit 13: the ring kernel's 192-row tiles where eligible
-  d.x3 = (epi >> 16) & 1;           // epi bit 16: f32x ring plans at tile N 128 on the plane-stacked kernel
+  d.x3 = (epi >> 16) & 3;           // epi bits 16-17: f32x ring plans on the plane-stacked kernels (x3 option)
   d.epi.act = act;
   d.epi.aux = aux;
   d.epi.ld_aux = ld_aux;

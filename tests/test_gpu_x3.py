@@ -21,12 +21,14 @@ def _gemm(lib, M, N, K, A, at, Bm, bt, ldc, flags, act=0, aux=None):
     return C
 
 
-@pytest.mark.parametrize("tm", [256, 192])
+@pytest.mark.parametrize("tm", [256, 192, "w256"])
 @pytest.mark.parametrize("at,bt", [(0, 0), (1, 0), (0, 1), (1, 1)])
 @pytest.mark.parametrize("epi", [0, 1, 2], ids=["store", "act", "dact"])
 @pytest.mark.parametrize("M,N,K", [(12288, 500, 501), (600, 260, 300), (700, 130, 4099), (501, 500, 8192),
                                    (256, 128, 32), (300, 200, 10001)])
 def test_x3_gemm_matches_float64_and_ring(tm, at, bt, epi, M, N, K):
+    """tm 256 / 192: the tile-N-128 form (ring variant 11, x3 = 1); w256: the 256x256 form (ring
+    variant 12, x3 = 2; 192-row plans stay on the ring kernel)."""
     if tm == 192 and at:
         pytest.skip("192-row tiles need a k-contiguous A")
     lib = _lib.load()
@@ -40,9 +42,9 @@ def test_x3_gemm_matches_float64_and_ring(tm, at, bt, epi, M, N, K):
         Bm[:, K:] = 0
     ldc = r8(N)
     aux = torch.tanh(torch.randn(M, ldc, device="cuda", generator=g)) if epi == 2 else None
-    flags = epi | (2 << 4) | (11 << 8) | ((1 << 13) if tm == 192 else 0)
+    flags = epi | (2 << 4) | ((12 if tm == "w256" else 11) << 8) | ((1 << 13) if tm == 192 else 0)
     Cr = _gemm(lib, M, N, K, A, at, Bm, bt, ldc, flags, 0, aux)
-    Cx = _gemm(lib, M, N, K, A, at, Bm, bt, ldc, flags | (1 << 16), 0, aux)
+    Cx = _gemm(lib, M, N, K, A, at, Bm, bt, ldc, flags | ((2 if tm == "w256" else 1) << 16), 0, aux)
     Ad = (A[:, :M].T if at else A[:, :K]).double()
     Bd = (Bm[:, :K].T if bt else Bm[:, :N]).double()
     acc = Ad @ Bd
@@ -58,15 +60,17 @@ def test_x3_gemm_matches_float64_and_ring(tm, at, bt, epi, M, N, K):
     assert (Cx[:, :N].double() - Cr[:, :N].double()).abs().max().item() <= 1e-6 * mag + 1e-7
 
 
-def test_x3_c2_step_vs_oracle():
+@pytest.mark.parametrize("x3", [1, 2])
+def test_x3_c2_step_vs_oracle(x3):
     """C2 (f32x) with x3: losses, gradients and the post-Adam parameters against the float64 oracle
     at the f32x bars of the other C2 step tests."""
     from magic_amd.config import baseline_config
     from tests.test_gpu_parity import check_step
-    check_step(baseline_config("C2").replace(options="x3=1"), adam=True)
+    check_step(baseline_config("C2").replace(options=f"x3={x3}"), adam=True)
 
 
-def test_x3_c2_steps_match_ring_kernel():
+@pytest.mark.parametrize("x3", [1, 2])
+def test_x3_c2_steps_match_ring_kernel(x3):
     """C2 with and without x3 on the same inputs: both gradients of one backward to fp32 rounding
     (the same plane products summed in another order), and the losses of three training steps (the
     second batch grey). Parameters are not compared bitwise-close: TF-Adam's m / sqrt(v) turns a
@@ -80,7 +84,7 @@ def test_x3_c2_steps_match_ring_kernel():
     P = make_params(cfg)
     batches = _batches(cfg, 3, 1, 17)
     res = []
-    for opt in ("x3=0", "x3=1"):
+    for opt in ("x3=0", f"x3={x3}"):
         eng = Engine(cfg.replace(options=opt), 0)
         try:
             eng.load_params(P)

@@ -1,6 +1,13 @@
 #!/bin/bash
-# r6zo: the de-interleave right after a 1 ms bf16 GEMM on random operands (+2000) or a 1 GB memset
-# (+4000), each launch timed alone, against back-to-back launches -- why the in-step pass is slower
+# r6zp: the 256x256 plane-stacked form (x3=2: C2's hidden weight gradients) -- tests, C2 A/B
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+T="python -u -m pytest -q -x --timeout 300 --timeout-method thread -p no:cacheprovider"
+A="--no-cpu-baseline --pmc off --no-h2d --no-pipeline --no-configs --steps 60 --warmup 5"
 bash tools/gpu_steps.sh \
-  "r6zo_db|400|python tools/deint_bench.py --config C3 --variants 7,2007,4007,1007,3007,5007 --rounds 3 --iters 10 && python tools/deint_bench.py --config C2 --variants 0,2000,4000 --rounds 3 --iters 10"
+  "r6zp_tx|600|$T -m gpu tests/test_gpu_x3.py" \
+  "r6zp_c2_1|200|python bench.py --config C2 $A --create-opt x3=1" \
+  "r6zp_c2_2|200|python bench.py --config C2 $A --create-opt x3=2" \
+  "r6zp_c2_1b|200|python bench.py --config C2 $A --create-opt x3=1" \
+  "r6zp_c2_2b|200|python bench.py --config C2 $A --create-opt x3=2" \
+  "r6zp_c2_1c|200|python bench.py --config C2 $A --create-opt x3=1" \
+  "r6zp_c2_2c|200|python bench.py --config C2 $A --create-opt x3=2"
