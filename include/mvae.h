@@ -142,8 +142,9 @@ int mvae_create(const mvae_cfg* cfg, int device, mvae_ctx** out);
  * kernel's s_setprio form, default 0), deint_variant (0-6 or 8, A/B: the de-interleave's form; 8 = coalesced X loads through LDS), cs_one
  * (0-2: the cosine metric's column statistics in one launch, the last row chunk's workgroup
  * summing the partials in the two-launch order -- the same bits; 2, the default: where L <= 32),
- * x3 (0/1: f32x ring-kernel plans at tile N 128 on the plane-stacked kernel, every operand plane
- * of a 32-k tile in LDS at once; the same products summed in another order; default 1). Diagnostics, results
+ * x3 (0-2: f32x ring-kernel plans on the plane-stacked kernels, every operand plane of a k-tile in
+ * LDS at once -- 1 the tile-N-128 plans, 2 also the 256x256 ones; the same products summed in
+ * another order; default 2). Diagnostics, results
  * meaningless: deint_fuse_diag (0-31: parts of the fused launch switched off), diag_skip_deint (1: de-interleave only the first batch -- a timing bound),
  * diag_shadow_deint (-1 or a workgroup count > 0: a second de-interleave of each step's input
  * into a scratch image on a low-priority stream, launched at diag_shadow_at = 0 the forward,

@@ -475,8 +475,9 @@ struct CreateOpts {
   int adam_nt = 1;      // Adam's moment / fp32 parameter stores non-temporal (C2 -0.6 %, C3 -0.3 %, r6za)
   int deint_variant = 0;  // the bits de-interleave's form (launch_deint_bits; diagnostics / A-B)
   int e8_prio = 0;      // the eight-phase kernel's s_setprio form (PParams::prio; A-B)
-  int x3 = 1;           // f32x: ring plans at tile N 128 on the plane-stacked kernel (gemm_bf16.hip;
-                        // C2 -2.1 / -2.9 % on two boxes, r6zi / r6zj)
+  int x3 = 2;           // f32x: ring plans on the plane-stacked kernels (gemm_bf16.hip): 1 the tile-N-128
+                        // plans (C2 -2.1 / -2.9 % on two boxes, r6zi / r6zj), 2 also the 256x256 ones
+                        // (C2's hidden weight gradients 68.5 -> 66.5 us, step -0.2 %, r6zp)
   int cs_one = 2;       // the column statistics in one launch (the last chunk's workgroup sums the
                         // partials in colstats_final_kernel's order: the same bits): 0 off, 1 on, 2
                         // where L <= 32 (one 64-column block: C2 -0.9 %; C3, L 200: +0.2 %, r6zh / r6zi)
